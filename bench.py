@@ -1,0 +1,280 @@
+#!/usr/bin/env python3
+"""Benchmark of the PWC-Net hot path on MI355X (BASELINE.json config 2 / config 3).
+
+One step = one pass of the hot path over one batch of synthetic 384x448 image pairs: for every
+pyramid level the reference's forward visits (model.py:72-113 at output_level=4: l0..l4 =
+192x6x7, 128x12x14, 96x24x28, 64x48x56, 32x96x112 at 384x448), the WarpingLayer
+(modules.py:31-42) warps the second image's features by the level's flow and the
+Correlation of model.py:24 (pad 9, k 1, md 9, s1 1, s2 2: 81 channels) correlates them with
+the first image's features.  Per GPU the batch is 8 pairs (config 2); with --gpus N every
+rank processes its own 8 pairs (config 3: 64 pairs over 8 GPUs), no collective on the data
+path ("scaling": "weak").
+
+Timed region: levels l0..l3 and the l4 warp are replayed from a hipGraph (one per rotating
+buffer set); the l4 correlation -- the dominant kernel, priced for the roofline -- is launched
+directly through the C ABI between two HIP events on the same stream, so its duration is
+measured live in every timed step.  Inputs rotate over enough buffer sets (> 2x the 256 MiB
+Infinity Cache) that each step reads them from HBM.
+
+cpu_baseline: the fp32 CPU port of the same path (oracle/pwc_oracle.c, OpenMP) on the same
+workload, rank 0 at N=1 only, timed for ~10 s.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pwc-net_pytorch_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# reference defaults (main.py:42-81): lv_chs, num_levels=7, output_level=4, search_range=4
+LV_CHS = [16, 32, 64, 96, 128, 192]
+NUM_LEVELS = 7
+OUTPUT_LEVEL = 4
+SEARCH_RANGE = 4
+CORR_ARGS = dict(pad_size=2 * SEARCH_RANGE + 1, kernel_size=1,
+                 max_displacement=2 * SEARCH_RANGE + 1, stride1=1, stride2=2)  # model.py:24
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def level_shapes(H, W):
+    """(C, h, w) of the correlated levels l = 0..output_level (model.py:72)."""
+    chs = LV_CHS[::-1]
+    out = []
+    for l in range(OUTPUT_LEVEL + 1):
+        s = 2 ** (NUM_LEVELS - 1 - l)
+        out.append((chs[l], H // s, W // s))
+    return out
+
+
+def corr_bytes_per_pair(C, h, w, elem=4):
+    """(2*C*H*W + 81*H*W) * sizeof -- read f1, read warped f2, write volume."""
+    return (2 * C * h * w + 81 * h * w) * elem
+
+
+def make_set(shapes, B, dev, dtype, gen):
+    s = []
+    for (C, h, w) in shapes:
+        x1 = torch.randn(B, C, h, w, device=dev, generator=gen).to(dtype)
+        x2 = torch.randn(B, C, h, w, device=dev, generator=gen).to(dtype)
+        flow = (torch.randn(B, 2, h, w, device=dev, generator=gen) * 2.0).to(dtype)
+        corr = torch.empty(B, 81, h, w, device=dev, dtype=dtype)
+        s.append(dict(x1=x1, x2=x2, flow=flow, corr=corr))
+    return s
+
+
+def cpu_baseline(shapes, B, seconds, threads):
+    from oracle import oracle as O
+    rng = np.random.default_rng(0)
+    data = []
+    for (C, h, w) in shapes:
+        data.append((rng.standard_normal((B, C, h, w)).astype(np.float32),
+                     rng.standard_normal((B, C, h, w)).astype(np.float32),
+                     (rng.standard_normal((B, 2, h, w)) * 2).astype(np.float32)))
+    O.set_num_threads(threads, np.float32)
+    used = O.num_threads(np.float32)
+
+    def one():
+        for x1, x2, fl in data:
+            w = O.warp_forward(x2, fl, dtype=np.float32)
+            O.corr_forward(x1, w, 9, 1, 9, 1, 2, dtype=np.float32)
+
+    one()  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 2000:
+            break
+    return dict(value=reps * B / el, unit="image-pairs/s", cores=used, kind="port",
+                sample=f"{reps} reps x {B} pairs of the same workload (warp + Corr9 at l0-l4, "
+                       f"384x448 pyramid shapes), fp32 oracle/pwc_oracle.c with {used} OpenMP "
+                       f"threads, {el:.1f} s")
+
+
+def load_pmc_traffic(path):
+    """HBM bytes per launch of the l4 correlation from a committed rocprofv3 PMC summary."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU")
+    ap.add_argument("--height", type=int, default=384)
+    ap.add_argument("--width", type=int, default=448)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "fp16"])
+    ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_l4corr_pmc.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import warp_forward, corr_forward
+    lib = _lib.load()
+
+    dtype = torch.float32 if args.dtype == "fp32" else torch.float16
+    esz = 4 if dtype == torch.float32 else 2
+    B = args.batch
+    shapes = level_shapes(args.height, args.width)
+    per_set = sum((2 * C * h * w + 2 * h * w + 81 * h * w + C * h * w) * B * esz
+                  for C, h, w in shapes)
+    nsets = args.sets or max(2, int(np.ceil(2 * 256 * 2 ** 20 / per_set)))
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    sets = [make_set(shapes, B, dev, dtype, gen) for _ in range(nsets)]
+    stream = torch.cuda.current_stream(dev)
+
+    # l4 correlation: direct C-ABI launch with pre-bound arguments
+    C4, h4, w4 = shapes[-1]
+    dcode = _lib.DTYPE_CODES[dtype]
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def corr_l4(s, x2w):
+        ret = lib.pwc_corr_forward(ctypes.c_void_p(s[-1]["x1"].data_ptr()),
+                                   ctypes.c_void_p(x2w.data_ptr()),
+                                   ctypes.c_void_p(s[-1]["corr"].data_ptr()), B, C4, h4, w4,
+                                   9, 1, 9, 1, 2, 1, dcode, sp)
+        if ret != 1:
+            _lib.check(ret, "bench corr_l4")
+
+    def pre(s):
+        """levels l0..l3 (warp + corr) and the l4 warp; returns the l4 warped features."""
+        for lv in s[:-1]:
+            w = warp_forward(lv["x2"], lv["flow"])
+            lv["corr"] = corr_forward(lv["x1"], w, **CORR_ARGS)
+        return warp_forward(s[-1]["x2"], s[-1]["flow"])
+
+    # warm the kernels (first-call attribute setup) before any capture
+    for s in sets:
+        corr_l4(s, pre(s))
+    torch.cuda.synchronize(dev)
+
+    graphs, warped = [], []
+    if not args.no_graph:
+        for s in sets:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                w = pre(s)
+            graphs.append(g)
+            warped.append(w)
+        torch.cuda.synchronize(dev)
+
+    def step(i, ev=None):
+        k = i % nsets
+        if graphs:
+            graphs[k].replay()
+            w = warped[k]
+        else:
+            w = pre(sets[k])
+        if ev is not None:
+            ev[0].record(stream)
+        corr_l4(sets[k], w)
+        if ev is not None:
+            ev[1].record(stream)
+
+    for i in range(args.warmup):
+        step(i)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    pairs = B * args.steps * world
+    value = pairs / elapsed
+    bytes_launch = corr_bytes_per_pair(C4, h4, w4, esz) * B
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic = load_pmc_traffic(args.pmc) if args.dtype == "fp32" and B == 8 else None
+
+    result = {
+        "metric": "image-pairs/sec (forward, 384x448): hot path = WarpingLayer + Correlation(d=4)"
+                  " at all 5 pyramid levels; lvl2 corr HBM GB/s vs peak",
+        "value": round(value, 2),
+        "unit": "image-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (randn features / N(0,2^2) flows of the pyramid shapes; no weights on "
+                "this path)",
+        "config": {
+            "workload": "BASELINE config 2 (config 3 at N>1): B=8 pairs/GPU, 384x448, warp + "
+                        "Correlation(pad 9, k 1, md 9, s1 1, s2 2) at levels l0-l4",
+            "global_batch": B * world,
+            "per_gpu_batch": B,
+            "height": args.height,
+            "width": args.width,
+            "levels": [list(s) for s in shapes],
+            "parallelism": f"dp{world} (batch-sharded replicas, no data-path collective)",
+            "buffer_sets": nsets,
+            "graph": bool(graphs),
+        },
+        "roofline": {
+            "kernel": "corr_fwd_tiled<Corr9> at l4 (32x96x112, B=8)",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "avg_launch_us": round(kern_ms * 1e3, 3),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(
+            16, len(os.sched_getaffinity(0)))
+        result["cpu_baseline"] = cpu_baseline(shapes, B, args.cpu_seconds, threads)
+        result["cpu_baseline"]["speedup"] = round(value / result["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+/*
+ * pwc_hotpath.h — C ABI of the MI355X (gfx950) PWC-Net hot path:
+ * cost-volume correlation, CostVolumeLayer-ordered cost volume and bilinear flow warp.
+ *
+ * Plain pointers and sizes only: no torch / THC types.  Every tensor is a caller-owned,
+ * contiguous NCHW device buffer (hipMalloc'd or torch-allocated) of the element type named
+ * by `dtype`.  `stream` is a hipStream_t (NULL = the legacy default stream).  All calls are
+ * asynchronous on `stream`, perform no host synchronisation and no allocation, so they may
+ * be captured into a hipGraph.
+ *
+ * Return value mirrors the reference launcher (correlation_cuda_kernel.cu:361-368):
+ *   1 = kernels enqueued, 0 = error (argument check or launch failure); the message is then
+ *   available from pwc_last_error() (thread-local).  The reference turned 0 into
+ *   THError("aborting") (correlation_cuda.c:86-89); the Python layer raises RuntimeError.
+ *
+ * Reference interfaces replaced (paths relative to daigo0927/PWC-Net_pytorch):
+ *   pwc_corr_output_shape  <- shape math of Correlation_forward_cuda, correlation_cuda.c:20-34
+ *   pwc_corr_forward       <- Correlation_forward_cuda (correlation_cuda.c:11-93, declared
+ *                             correlation_cuda.h:1-8) -> Correlation_forward_cuda_kernel
+ *                             (correlation_cuda_kernel.h:5-38, .cu:296-369).  No rInput1/
+ *                             rInput2 scratch: the NHWC transpose (cu:10-32) is not needed.
+ *   pwc_corr_backward      <- Correlation_backward_cuda (correlation_cuda.c:95-180,
+ *                             correlation_cuda.h:10-17) -> Correlation_backward_cuda_kernel
+ *                             (correlation_cuda_kernel.h:40-88, .cu:371-473)
+ *   pwc_cost_volume_forward/backward <- CostVolumeLayer.forward (modules.py:53-74) and its
+ *                             autograd; there is no C interface in the reference (pure ATen).
+ *   pwc_warp_forward/backward <- WarpingLayer.forward (modules.py:31-42) + get_grid
+ *                             (utils.py:3-8) + F.grid_sample/grid_sampler_2d_backward with
+ *                             torch-0.4 semantics (bilinear, zeros, align_corners=True).
+ */
+#ifndef PWC_HOTPATH_H
+#define PWC_HOTPATH_H
+
+#if defined(__GNUC__) || defined(__clang__)
+#define PWC_API __attribute__((visibility("default")))
+#else
+#define PWC_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types (`dtype` arguments).  Arithmetic is always fp32 accumulate. */
+#define PWC_DTYPE_F32 0
+#define PWC_DTYPE_F16 1
+#define PWC_DTYPE_BF16 2
+
+/* ABI version; bumped on any signature change. */
+PWC_API int pwc_abi_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+PWC_API const char* pwc_last_error(void);
+
+/* correlation_cuda.c:20-34: OC = ((md/s2)*2+1)^2, Ho = ceil((H+2pad-2(kr+md))/s1), Wo alike,
+ * kr = (k-1)/2 (C truncation).  Returns 0 if the output would be empty. */
+PWC_API int pwc_corr_output_shape(int H, int W, int pad_size, int kernel_size, int max_displacement,
+                          int stride1, int stride2, int* out_channels, int* out_height,
+                          int* out_width);
+
+/* out[B][OC][Ho][Wo] = correlation of in1, in2 ([B][C][H][W]) exactly as
+ * correlation_cuda_kernel.cu:34-106: channel tc = (tj+dr)*D + (ti+dr), value divided by
+ * kernel_size^2 * C.  corr_multiply is accepted and ignored, as in the reference. */
+PWC_API int pwc_corr_forward(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
+                     int pad_size, int kernel_size, int max_displacement, int stride1,
+                     int stride2, int corr_multiply, int dtype, void* stream);
+
+/* grad_in1/grad_in2 ([B][C][H][W]) from grad_out ([B][OC][Ho][Wo]) exactly as
+ * correlation_cuda_kernel.cu:108-290.  Requires stride1 == 1 (the reference backward is
+ * undefined otherwise: it indexes gradInput with the strided coordinate).  Every element of
+ * both gradients is written (no pre-zeroing needed). */
+PWC_API int pwc_corr_backward(const void* in1, const void* in2, const void* grad_out, void* grad_in1,
+                      void* grad_in2, int B, int C, int H, int W, int pad_size,
+                      int kernel_size, int max_displacement, int stride1, int stride2,
+                      int corr_multiply, int dtype, void* stream);
+
+/* CostVolumeLayer (modules.py:53-74): out[B][(2sr+1)^2][H][W], channel order of
+ * modules.py:58-72, value sum_c src*tgt(shifted) / (2sr+1)^2. */
+PWC_API int pwc_cost_volume_forward(const void* src, const void* tgt, void* out, int B, int C, int H,
+                            int W, int search_range, int dtype, void* stream);
+PWC_API int pwc_cost_volume_backward(const void* src, const void* tgt, const void* grad_out,
+                             void* grad_src, void* grad_tgt, int B, int C, int H, int W,
+                             int search_range, int dtype, void* stream);
+
+/* WarpingLayer: out[b][c][y][x] = bilinear sample of x at (x + u, y + v) with the reference's
+ * normalisation chain (flow / ((W-1)/2) + linspace(-1,1), align_corners=True), zeros outside.
+ * flow is [B][2][H][W], channel 0 = u (horizontal), 1 = v (vertical), in pixels. */
+PWC_API int pwc_warp_forward(const void* x, const void* flow, void* out, int B, int C, int H, int W,
+                     int dtype, void* stream);
+/* grad_x is zeroed on `stream` and accumulated with fp32 atomics (as ATen's
+ * grid_sampler_2d_backward); grad_flow is written element-wise. */
+PWC_API int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, void* grad_x,
+                      void* grad_flow, int B, int C, int H, int W, int dtype, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PWC_HOTPATH_H */

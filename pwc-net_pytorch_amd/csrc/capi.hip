@@ -1,0 +1,271 @@
+// capi.hip — the extern "C" boundary declared in include/pwc_hotpath.h.
+//
+// Argument checks mirror what the reference enforced or silently assumed
+// (correlation_package/functions/correlation.py:17-18 contiguity asserts are done by the
+// Python layer; correlation_cuda.c:20-42 shape math and fills; cu:361-368 launch check).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/pwc_hotpath.h"
+#include "pwc_common.cuh"
+
+namespace pwc {
+template <typename T>
+hipError_t corr_forward_t(const void*, const void*, void*, int, int, int, int, int, int, int,
+                          int, int, int, int, int, float, hipStream_t, int);
+template <typename T>
+hipError_t corr_backward_t(const void*, const void*, const void*, void*, void*, int, int, int,
+                           int, int, int, int, int, int, int, int, int, float, hipStream_t,
+                           int);
+template <typename T>
+hipError_t warp_forward_t(const void*, const void*, void*, int, int, int, int, hipStream_t);
+hipError_t warp_backward_f32(const void*, const void*, const void*, void*, void*, int, int, int,
+                             int, hipStream_t);
+}  // namespace pwc
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(const char* fn, const char* msg) {
+  std::snprintf(g_err, sizeof(g_err), "%s: %s", fn, msg);
+  return 0;
+}
+
+int check_launch(const char* fn, hipError_t e) {
+  if (e != hipSuccess) {
+    std::snprintf(g_err, sizeof(g_err), "%s: launch failed: %s", fn, hipGetErrorString(e));
+    return 0;
+  }
+  g_err[0] = '\0';
+  return 1;
+}
+
+bool dims_ok(int B, int C, int H, int W) { return B >= 0 && C >= 0 && H >= 0 && W >= 0; }
+
+// correlation_cuda.c:20-34
+bool corr_shape(int H, int W, int pad, int k, int md, int s1, int s2, int* oc, int* oh,
+                int* ow) {
+  if (s1 <= 0 || s2 <= 0 || k < 0 || md < 0 || pad < 0) return false;
+  const int kr = (k - 1) / 2;
+  const int br = kr + md;
+  const int pH = H + 2 * pad, pW = W + 2 * pad;
+  const int dr = md / s2;
+  *oc = (2 * dr + 1) * (2 * dr + 1);
+  *oh = (int)std::ceil((float)(pH - 2 * br) / (float)s1);
+  *ow = (int)std::ceil((float)(pW - 2 * br) / (float)s1);
+  return true;
+}
+
+// FORCE_GENERIC (env PWC_FORCE_GENERIC=1) routes correlation to the generic kernels; used by
+// the parity tests to cross-check the tiled kernels against the literal restatement.
+int force_generic() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = std::getenv("PWC_FORCE_GENERIC");
+    v = (s && s[0] == '1') ? 1 : 0;
+  }
+  return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pwc_abi_version(void) { return 1; }
+
+const char* pwc_last_error(void) { return g_err; }
+
+int pwc_corr_output_shape(int H, int W, int pad_size, int kernel_size, int max_displacement,
+                          int stride1, int stride2, int* out_channels, int* out_height,
+                          int* out_width) {
+  if (!out_channels || !out_height || !out_width)
+    return fail("pwc_corr_output_shape", "null output pointer");
+  if (!corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2,
+                  out_channels, out_height, out_width))
+    return fail("pwc_corr_output_shape", "invalid correlation parameters");
+  if (*out_height <= 0 || *out_width <= 0)
+    return fail("pwc_corr_output_shape", "empty correlation output");
+  return 1;
+}
+
+int pwc_corr_forward(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
+                     int pad_size, int kernel_size, int max_displacement, int stride1,
+                     int stride2, int corr_multiply, int dtype, void* stream) {
+  (void)corr_multiply;  // ignored by the reference kernels as well
+  const char* fn = "pwc_corr_forward";
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (!corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo))
+    return fail(fn, "invalid correlation parameters");
+  if (Ho <= 0 || Wo <= 0) return fail(fn, "empty correlation output");
+  if ((size_t)B * C * H * W && (!in1 || !in2 || !out)) return fail(fn, "null buffer");
+  const float divisor = (float)(kernel_size * kernel_size * C);  // cu:65 nelems
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case PWC_DTYPE_F32:
+      e = pwc::corr_forward_t<float>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size, kernel_size,
+                                     max_displacement, stride1, stride2, pwc::kRaster, divisor,
+                                     s, force_generic());
+      break;
+    case PWC_DTYPE_F16:
+      e = pwc::corr_forward_t<__half>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size, kernel_size,
+                                      max_displacement, stride1, stride2, pwc::kRaster,
+                                      divisor, s, force_generic());
+      break;
+    case PWC_DTYPE_BF16:
+      e = pwc::corr_forward_t<__hip_bfloat16>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size,
+                                              kernel_size, max_displacement, stride1, stride2,
+                                              pwc::kRaster, divisor, s, force_generic());
+      break;
+    default:
+      return fail(fn, "unsupported dtype");
+  }
+  return check_launch(fn, e);
+}
+
+int pwc_corr_backward(const void* in1, const void* in2, const void* grad_out, void* grad_in1,
+                      void* grad_in2, int B, int C, int H, int W, int pad_size,
+                      int kernel_size, int max_displacement, int stride1, int stride2,
+                      int corr_multiply, int dtype, void* stream) {
+  (void)corr_multiply;
+  const char* fn = "pwc_corr_backward";
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (stride1 != 1)
+    return fail(fn, "stride1 != 1 is undefined in the reference backward (cu:120-121)");
+  if (!corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo))
+    return fail(fn, "invalid correlation parameters");
+  if (Ho <= 0 || Wo <= 0) return fail(fn, "empty correlation output");
+  if ((size_t)B * C * H * W && (!in1 || !in2 || !grad_out || !grad_in1 || !grad_in2))
+    return fail(fn, "null buffer");
+  const float divisor = (float)(kernel_size * kernel_size * C);
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case PWC_DTYPE_F32:
+      e = pwc::corr_backward_t<float>(in1, in2, grad_out, grad_in1, grad_in2, B, C, H, W, Ho,
+                                      Wo, pad_size, kernel_size, max_displacement, stride1,
+                                      stride2, pwc::kRaster, divisor, s, force_generic());
+      break;
+    case PWC_DTYPE_F16:
+      e = pwc::corr_backward_t<__half>(in1, in2, grad_out, grad_in1, grad_in2, B, C, H, W, Ho,
+                                       Wo, pad_size, kernel_size, max_displacement, stride1,
+                                       stride2, pwc::kRaster, divisor, s, force_generic());
+      break;
+    case PWC_DTYPE_BF16:
+      e = pwc::corr_backward_t<__hip_bfloat16>(in1, in2, grad_out, grad_in1, grad_in2, B, C, H,
+                                               W, Ho, Wo, pad_size, kernel_size,
+                                               max_displacement, stride1, stride2,
+                                               pwc::kRaster, divisor, s, force_generic());
+      break;
+    default:
+      return fail(fn, "unsupported dtype");
+  }
+  return check_launch(fn, e);
+}
+
+int pwc_cost_volume_forward(const void* src, const void* tgt, void* out, int B, int C, int H,
+                            int W, int search_range, int dtype, void* stream) {
+  const char* fn = "pwc_cost_volume_forward";
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (search_range < 0) return fail(fn, "negative search_range");
+  if ((size_t)B * C * H * W && (!src || !tgt || !out)) return fail(fn, "null buffer");
+  const int K = (2 * search_range + 1) * (2 * search_range + 1);
+  const float divisor = (float)K;  // modules.py:74 output / shape[1]
+  const int sr = search_range;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  // CostVolumeLayer == Correlation(pad=sr, k=1, md=sr, s1=1, s2=1) with CVL channel order.
+  switch (dtype) {
+    case PWC_DTYPE_F32:
+      e = pwc::corr_forward_t<float>(src, tgt, out, B, C, H, W, H, W, sr, 1, sr, 1, 1,
+                                     pwc::kCvl, divisor, s, force_generic());
+      break;
+    case PWC_DTYPE_F16:
+      e = pwc::corr_forward_t<__half>(src, tgt, out, B, C, H, W, H, W, sr, 1, sr, 1, 1,
+                                      pwc::kCvl, divisor, s, force_generic());
+      break;
+    case PWC_DTYPE_BF16:
+      e = pwc::corr_forward_t<__hip_bfloat16>(src, tgt, out, B, C, H, W, H, W, sr, 1, sr, 1, 1,
+                                              pwc::kCvl, divisor, s, force_generic());
+      break;
+    default:
+      return fail(fn, "unsupported dtype");
+  }
+  return check_launch(fn, e);
+}
+
+int pwc_cost_volume_backward(const void* src, const void* tgt, const void* grad_out,
+                             void* grad_src, void* grad_tgt, int B, int C, int H, int W,
+                             int search_range, int dtype, void* stream) {
+  const char* fn = "pwc_cost_volume_backward";
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (search_range < 0) return fail(fn, "negative search_range");
+  if ((size_t)B * C * H * W && (!src || !tgt || !grad_out || !grad_src || !grad_tgt))
+    return fail(fn, "null buffer");
+  const int K = (2 * search_range + 1) * (2 * search_range + 1);
+  const float divisor = (float)K;
+  const int sr = search_range;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case PWC_DTYPE_F32:
+      e = pwc::corr_backward_t<float>(src, tgt, grad_out, grad_src, grad_tgt, B, C, H, W, H, W,
+                                      sr, 1, sr, 1, 1, pwc::kCvl, divisor, s, force_generic());
+      break;
+    case PWC_DTYPE_F16:
+      e = pwc::corr_backward_t<__half>(src, tgt, grad_out, grad_src, grad_tgt, B, C, H, W, H,
+                                       W, sr, 1, sr, 1, 1, pwc::kCvl, divisor, s,
+                                       force_generic());
+      break;
+    case PWC_DTYPE_BF16:
+      e = pwc::corr_backward_t<__hip_bfloat16>(src, tgt, grad_out, grad_src, grad_tgt, B, C, H,
+                                               W, H, W, sr, 1, sr, 1, 1, pwc::kCvl, divisor, s,
+                                               force_generic());
+      break;
+    default:
+      return fail(fn, "unsupported dtype");
+  }
+  return check_launch(fn, e);
+}
+
+int pwc_warp_forward(const void* x, const void* flow, void* out, int B, int C, int H, int W,
+                     int dtype, void* stream) {
+  const char* fn = "pwc_warp_forward";
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if ((size_t)B * C * H * W && (!x || !flow || !out)) return fail(fn, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case PWC_DTYPE_F32:
+      e = pwc::warp_forward_t<float>(x, flow, out, B, C, H, W, s);
+      break;
+    case PWC_DTYPE_F16:
+      e = pwc::warp_forward_t<__half>(x, flow, out, B, C, H, W, s);
+      break;
+    case PWC_DTYPE_BF16:
+      e = pwc::warp_forward_t<__hip_bfloat16>(x, flow, out, B, C, H, W, s);
+      break;
+    default:
+      return fail(fn, "unsupported dtype");
+  }
+  return check_launch(fn, e);
+}
+
+int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, void* grad_x,
+                      void* grad_flow, int B, int C, int H, int W, int dtype, void* stream) {
+  const char* fn = "pwc_warp_backward";
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (dtype != PWC_DTYPE_F32) return fail(fn, "backward is fp32 only");
+  if ((size_t)B * H * W && (!x || !flow || !grad_out || !grad_x || !grad_flow))
+    return fail(fn, "null buffer");
+  return check_launch(fn, pwc::warp_backward_f32(x, flow, grad_out, grad_x, grad_flow, B, C, H,
+                                                 W, (hipStream_t)stream));
+}
+
+}  // extern "C"

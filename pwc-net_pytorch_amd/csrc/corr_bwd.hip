@@ -1,0 +1,199 @@
+// corr_bwd.hip — cost-volume correlation backward for gfx950, as gathers (no atomics).
+//
+// Semantics: correlation_cuda_kernel.cu:108-198 (grad input1) and :200-290 (grad input2)
+// of daigo0927/PWC-Net_pytorch, defined there for stride1 == 1 only.  With k == 1 and
+// off = max_displacement - pad_size:
+//   g1[n,c,y,x] = 1/(k*k*C) * sum_tc gO[n,tc,y-off,x-off] * f2[n,c,y+dy_tc,x+dx_tc]
+//   g2[n,c,y,x] = 1/(k*k*C) * sum_tc gO[n,tc,y-off-dy_tc,x-off-dx_tc] * f1[n,c,y-dy_tc,x-dx_tc]
+// (terms whose output position lies outside [0,Ho)x[0,Wo), or whose feature position lies
+// outside the image, are zero), (dy,dx)_tc = ((tc/D-dr)*s2, (tc%D-dr)*s2).  The reference
+// launches B separate grids per gradient (cu:441-463); here one launch covers the batch.
+//
+// k == 1 kernel: one thread per pixel and CB channels: each gO value is loaded once per
+// displacement and reused across the CB channels held in registers; loads are coalesced
+// along W.  Generic kernel: literal cu:119-196 / cu:211-288 loops (any k, s1 == 1).
+#include "pwc_common.cuh"
+
+namespace pwc {
+
+template <typename T, int CB, int GRAD>  // GRAD 1: d/d input1, 2: d/d input2
+__global__ __launch_bounds__(256) void corr_bwd_k1(
+    const T* __restrict__ in1, const T* __restrict__ in2, const T* __restrict__ gout,
+    T* __restrict__ gin, int B, int C, int H, int W, int Ho, int Wo, int off, int dr, int s2,
+    int layout, float divisor) {
+  const int D = 2 * dr + 1, OC = D * D;
+  const int ncb = (C + CB - 1) / CB;
+  const size_t npix = (size_t)B * H * W;
+  const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const int cb = blockIdx.y;
+  if (idx >= npix || cb >= ncb) return;
+  const int x = idx % W;
+  const int y = (idx / W) % H;
+  const int n = idx / ((size_t)W * H);
+  const int c0 = cb * CB;
+  const size_t plane = (size_t)H * W;
+  const size_t oplane = (size_t)Ho * Wo;
+  const T* go_n = gout + (size_t)n * OC * oplane;
+
+  float acc[CB];
+#pragma unroll
+  for (int i = 0; i < CB; ++i) acc[i] = 0.f;
+
+  if (GRAD == 1) {
+    const int oy = y - off, ox = x - off;
+    if (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo) {
+      const T* f2n = in2 + (size_t)n * C * plane;
+      for (int tj = -dr; tj <= dr; ++tj) {
+        const int yy = y + tj * s2;
+        if (yy < 0 || yy >= H) continue;
+        for (int ti = -dr; ti <= dr; ++ti) {
+          const int xx = x + ti * s2;
+          if (xx < 0 || xx >= W) continue;
+          const int oc = out_channel(layout, tj, ti, dr, D, s2);
+          const float g = to_f32(go_n[(size_t)oc * oplane + (size_t)oy * Wo + ox]);
+          const T* f = f2n + (size_t)yy * W + xx;
+#pragma unroll
+          for (int i = 0; i < CB; ++i)
+            if (c0 + i < C) acc[i] = fmaf(g, to_f32(f[(size_t)(c0 + i) * plane]), acc[i]);
+        }
+      }
+    }
+  } else {
+    const T* f1n = in1 + (size_t)n * C * plane;
+    for (int tj = -dr; tj <= dr; ++tj) {
+      const int yy = y - tj * s2;  // f1 row paired with this f2 pixel
+      const int oy = yy - off;
+      if (yy < 0 || yy >= H || oy < 0 || oy >= Ho) continue;
+      for (int ti = -dr; ti <= dr; ++ti) {
+        const int xx = x - ti * s2;
+        const int ox = xx - off;
+        if (xx < 0 || xx >= W || ox < 0 || ox >= Wo) continue;
+        const int oc = out_channel(layout, tj, ti, dr, D, s2);
+        const float g = to_f32(go_n[(size_t)oc * oplane + (size_t)oy * Wo + ox]);
+        const T* f = f1n + (size_t)yy * W + xx;
+#pragma unroll
+        for (int i = 0; i < CB; ++i)
+          if (c0 + i < C) acc[i] = fmaf(g, to_f32(f[(size_t)(c0 + i) * plane]), acc[i]);
+      }
+    }
+  }
+  T* gn = gin + (size_t)n * C * plane + (size_t)y * W + x;
+#pragma unroll
+  for (int i = 0; i < CB; ++i)
+    if (c0 + i < C) gn[(size_t)(c0 + i) * plane] = from_f32<T>(acc[i] / divisor);
+}
+
+// Literal restatement of cu:119-196 and cu:211-288 (stride1 == 1), one thread per element.
+template <typename T>
+__global__ void corr_bwd_generic(const T* __restrict__ in1, const T* __restrict__ in2,
+                                 const T* __restrict__ gout, T* __restrict__ g1,
+                                 T* __restrict__ g2, int B, int C, int H, int W, int Ho, int Wo,
+                                 int pad, int kr, int md, int s1, int s2, int dr, int layout,
+                                 float divisor) {
+  const int D = 2 * dr + 1, OC = D * D;
+  const size_t total = (size_t)B * C * H * W;
+  const size_t plane = (size_t)H * W;
+  const size_t oplane = (size_t)Ho * Wo;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int col = idx % W;
+    const int row = (idx / W) % H;
+    const int c = (idx / plane) % C;
+    const int n = idx / (plane * C);
+    const int y = row * s1 + pad, x = col * s1 + pad;  // padded coordinates
+    const T* go_n = gout + (size_t)n * OC * oplane;
+    // ---- grad input1 ----
+    {
+      int xmin = (x - kr - md) / s1, ymin = (y - kr - md) / s1;
+      int xmax = (x + kr - md) / s1, ymax = (y + kr - md) / s1;
+      float sum = 0.f;
+      if (!(xmax < 0 || ymax < 0 || xmin >= Wo || ymin >= Ho) && !(xmin > xmax || ymin > ymax)) {
+        xmin = max(0, xmin);
+        xmax = min(Wo - 1, xmax);
+        ymin = max(0, ymin);
+        ymax = min(Ho - 1, ymax);
+        for (int tc = 0; tc < OC; ++tc) {
+          const int i2 = (tc % D - dr) * s2, j2 = (tc / D - dr) * s2;
+          const int yy = y + j2 - pad, xx = x + i2 - pad;
+          const float val2 = (yy >= 0 && yy < H && xx >= 0 && xx < W)
+                                 ? to_f32(in2[((size_t)n * C + c) * plane + (size_t)yy * W + xx])
+                                 : 0.f;
+          const int oc = layout == kCvl ? cvl_channel(j2, i2, dr) : tc;
+          for (int j = ymin; j <= ymax; ++j)
+            for (int i = xmin; i <= xmax; ++i)
+              sum += to_f32(go_n[(size_t)oc * oplane + (size_t)j * Wo + i]) * val2;
+        }
+      }
+      g1[idx] = from_f32<T>(sum / divisor);
+    }
+    // ---- grad input2 ----
+    {
+      float sum = 0.f;
+      for (int tc = 0; tc < OC; ++tc) {
+        const int i2 = (tc % D - dr) * s2, j2 = (tc / D - dr) * s2;
+        int xmin = (x - kr - md - i2) / s1, ymin = (y - kr - md - j2) / s1;
+        int xmax = (x + kr - md - i2) / s1, ymax = (y + kr - md - j2) / s1;
+        if (xmax < 0 || ymax < 0 || xmin >= Wo || ymin >= Ho) continue;
+        if (xmin > xmax || ymin > ymax) continue;
+        xmin = max(0, xmin);
+        xmax = min(Wo - 1, xmax);
+        ymin = max(0, ymin);
+        ymax = min(Ho - 1, ymax);
+        const int yy = y - j2 - pad, xx = x - i2 - pad;
+        const float val1 = (yy >= 0 && yy < H && xx >= 0 && xx < W)
+                               ? to_f32(in1[((size_t)n * C + c) * plane + (size_t)yy * W + xx])
+                               : 0.f;
+        const int oc = layout == kCvl ? cvl_channel(j2, i2, dr) : tc;
+        for (int j = ymin; j <= ymax; ++j)
+          for (int i = xmin; i <= xmax; ++i)
+            sum += to_f32(go_n[(size_t)oc * oplane + (size_t)j * Wo + i]) * val1;
+      }
+      g2[idx] = from_f32<T>(sum / divisor);
+    }
+  }
+}
+
+template <typename T>
+hipError_t corr_backward_t(const void* in1, const void* in2, const void* gout, void* g1,
+                           void* g2, int B, int C, int H, int W, int Ho, int Wo, int pad, int k,
+                           int md, int s1, int s2, int layout, float divisor,
+                           hipStream_t stream, int force_generic) {
+  const int kr = (k - 1) / 2;
+  const int dr = md / s2;
+  const size_t npix = (size_t)B * H * W;
+  if (npix == 0 || C == 0) return hipSuccess;
+  if (!force_generic && k == 1 && s1 == 1) {
+    constexpr int CB = 8;
+    const int off = md - pad;
+    dim3 grid((unsigned)((npix + 255) / 256), (unsigned)((C + CB - 1) / CB));
+    hipLaunchKernelGGL((corr_bwd_k1<T, CB, 1>), grid, dim3(256), 0, stream, (const T*)in1,
+                       (const T*)in2, (const T*)gout, (T*)g1, B, C, H, W, Ho, Wo, off, dr, s2,
+                       layout, divisor);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((corr_bwd_k1<T, CB, 2>), grid, dim3(256), 0, stream, (const T*)in1,
+                       (const T*)in2, (const T*)gout, (T*)g2, B, C, H, W, Ho, Wo, off, dr, s2,
+                       layout, divisor);
+    return hipGetLastError();
+  }
+  const size_t total = npix * C;
+  size_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(corr_bwd_generic<T>, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     (const T*)in1, (const T*)in2, (const T*)gout, (T*)g1, (T*)g2, B, C, H, W,
+                     Ho, Wo, pad, kr, md, s1, s2, dr, layout, divisor);
+  return hipGetLastError();
+}
+
+template hipError_t corr_backward_t<float>(const void*, const void*, const void*, void*, void*,
+                                           int, int, int, int, int, int, int, int, int, int,
+                                           int, int, float, hipStream_t, int);
+template hipError_t corr_backward_t<__half>(const void*, const void*, const void*, void*, void*,
+                                            int, int, int, int, int, int, int, int, int, int,
+                                            int, int, float, hipStream_t, int);
+template hipError_t corr_backward_t<__hip_bfloat16>(const void*, const void*, const void*,
+                                                    void*, void*, int, int, int, int, int, int,
+                                                    int, int, int, int, int, int, float,
+                                                    hipStream_t, int);
+
+}  // namespace pwc

@@ -1,0 +1,375 @@
+// corr_fwd.hip — cost-volume correlation forward for gfx950 (MI355X).
+//
+// Semantics: correlation_cuda_kernel.cu:34-106 of daigo0927/PWC-Net_pytorch (values),
+// correlation_cuda.c:20-34 (shapes).  For kernel_size == 1, stride1 == 1 the output pixel
+// (oy, ox) pairs f1 at (oy+off, ox+off) with f2 at (oy+off+tj*s2, ox+off+ti*s2),
+// off = max_displacement - pad_size, zero outside the image (the reference's zero-padded
+// NHWC scratch, cu:10-32, is never materialised here).
+//
+// Tiled kernel (k == 1, s1 == 1; template displacement radius DR and stride S):
+//   * one workgroup = one TY x TX output tile of one image, D*TY*NG threads
+//     (thread = output row ty, pixel group g, displacement row tj);
+//   * channels stream through a double-buffered LDS tile in chunks of CC: the f1 tile and
+//     the f2 tile with a DR*S halo are read from HBM once per workgroup, coalesced along W
+//     (float4 where aligned), and de-interleaved by x mod S so every lane's f2 window for
+//     its PX same-phase pixels is PX+2*DR contiguous floats (ds_read_b128, row stride 48
+//     dwords => conflict-free for the b128 lane groups);
+//   * each thread accumulates PX x D outputs in registers (fp32 FMA chain over C);
+//   * blocks are remapped XCD-aware so neighbouring tiles (shared halo rows) share an L2.
+// Generic kernel: any (pad, k, md, s1, s2), one thread per output element; used for the
+// rarely-used configurations the tiled kernel does not instantiate.
+#include "pwc_common.cuh"
+
+namespace pwc {
+
+template <int DR_, int S_, int GS_, int PX_, int NQ_, int TY_, int CC_>
+struct CorrTile {
+  static constexpr int DR = DR_, S = S_, GS = GS_, PX = PX_, NQ = NQ_, TY = TY_, CC = CC_;
+  static constexpr int D = 2 * DR + 1;
+  static constexpr int HALO = DR * S;
+  static constexpr int NG = GS * NQ;         // pixel groups per tile row
+  static constexpr int TX = NG * PX;         // tile width (pixels)
+  static constexpr int R2 = TY + 2 * HALO;   // f2 tile rows
+  static constexpr int X2 = TX + 2 * HALO;   // f2 tile columns
+  static constexpr int NW = (GS == S) ? PX + 2 * DR : PX + 2 * DR * S;  // f2 window / lane
+  static constexpr int THREADS = TY * NG * D;
+  // row strides (floats): f2 rows padded to 16 (mod 32) dwords so that the four rows a
+  // ds_read_b128 lane group touches land on disjoint 16-bank slices; f1 rows are 16 wide.
+  static constexpr int RS2 = ((X2 + 15) / 32) * 32 + 16;
+  static constexpr int RS1 = TX;
+  static constexpr int F2_FLOATS = CC * R2 * RS2;
+  static constexpr int F1_FLOATS = CC * TY * RS1;
+  static constexpr int BUF_FLOATS = F2_FLOATS + F1_FLOATS;
+  static constexpr int LDS_BYTES = 2 * BUF_FLOATS * 4;
+  static_assert(PX == 4, "lane windows are handled as float4 quads");
+  static_assert(GS == 1 || GS == S, "pixel grouping: consecutive or same-phase");
+  static_assert(X2 % (4 * GS) == 0, "f2 tile row must split into whole quads per phase");
+  static_assert(THREADS % 64 == 0, "whole wavefronts");
+  static_assert(THREADS <= 1024, "workgroup size");
+  static_assert(RS2 >= X2, "row stride");
+};
+
+// LDS float index of tile element (xh) within a row, layout [quad][phase][4].
+template <class G>
+__device__ __forceinline__ int lds_col(int xh) {
+  const int p = xh % G::GS;
+  const int m = xh / G::GS;
+  return ((m >> 2) * G::GS + p) * 4 + (m & 3);
+}
+
+template <class G, typename T>
+struct Stager {
+  // float4 "slots" of the f2 and f1 tiles for one channel chunk, spread over the block.
+  static constexpr int SLOTS2 = G::CC * G::R2 * (G::X2 / 4);
+  static constexpr int SLOTS1 = G::CC * G::TY * (G::TX / 4);
+  static constexpr int IT2 = (SLOTS2 + G::THREADS - 1) / G::THREADS;
+  static constexpr int IT1 = (SLOTS1 + G::THREADS - 1) / G::THREADS;
+  float4 r2[IT2];
+  float4 r1[IT1];
+
+  __device__ __forceinline__ static float4 load4(const T* __restrict__ base, int y, int x,
+                                                 int H, int W, bool vec_ok) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (y < 0 || y >= H) return v;
+    const T* row = base + (size_t)y * W;
+    if (vec_ok && x >= 0 && x + 3 < W) {
+      if constexpr (sizeof(T) == 4) {
+        v = *reinterpret_cast<const float4*>(row + x);
+      } else {
+        const uint2 raw = *reinterpret_cast<const uint2*>(row + x);
+        const T* h = reinterpret_cast<const T*>(&raw);
+        v = make_float4(to_f32(h[0]), to_f32(h[1]), to_f32(h[2]), to_f32(h[3]));
+      }
+      return v;
+    }
+    float e[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int xx = x + i;
+      e[i] = (xx >= 0 && xx < W) ? to_f32(row[xx]) : 0.f;
+    }
+    return make_float4(e[0], e[1], e[2], e[3]);
+  }
+
+  // Issue the global loads of chunk c0 (channels c0 .. c0+CC-1) into registers.
+  __device__ __forceinline__ void load(const T* __restrict__ f1n, const T* __restrict__ f2n,
+                                       int c0, int C, int H, int W, int y1, int x1,
+                                       bool vec_ok) {
+    const size_t plane = (size_t)H * W;
+#pragma unroll
+    for (int it = 0; it < IT2; ++it) {
+      const int s = threadIdx.x + it * G::THREADS;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (s < SLOTS2) {
+        const int q4 = s % (G::X2 / 4);
+        const int rr = (s / (G::X2 / 4)) % G::R2;
+        const int cc = s / ((G::X2 / 4) * G::R2);
+        const int c = c0 + cc;
+        if (c < C)
+          v = load4(f2n + (size_t)c * plane, y1 - G::HALO + rr, x1 - G::HALO + 4 * q4, H, W,
+                    vec_ok);
+      }
+      r2[it] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < IT1; ++it) {
+      const int s = threadIdx.x + it * G::THREADS;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (s < SLOTS1) {
+        const int q4 = s % (G::TX / 4);
+        const int rr = (s / (G::TX / 4)) % G::TY;
+        const int cc = s / ((G::TX / 4) * G::TY);
+        const int c = c0 + cc;
+        if (c < C) v = load4(f1n + (size_t)c * plane, y1 + rr, x1 + 4 * q4, H, W, vec_ok);
+      }
+      r1[it] = v;
+    }
+  }
+
+  // Scatter the registers into one LDS buffer in the de-interleaved [quad][phase][4] layout.
+  __device__ __forceinline__ void store(float* __restrict__ buf) const {
+    float* F2 = buf;
+    float* F1 = buf + G::F2_FLOATS;
+#pragma unroll
+    for (int it = 0; it < IT2; ++it) {
+      const int s = threadIdx.x + it * G::THREADS;
+      if (s < SLOTS2) {
+        const int q4 = s % (G::X2 / 4);
+        const int rr = (s / (G::X2 / 4)) % G::R2;
+        const int cc = s / ((G::X2 / 4) * G::R2);
+        float* row = F2 + (cc * G::R2 + rr) * G::RS2;
+        const float e[4] = {r2[it].x, r2[it].y, r2[it].z, r2[it].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[lds_col<G>(4 * q4 + i)] = e[i];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < IT1; ++it) {
+      const int s = threadIdx.x + it * G::THREADS;
+      if (s < SLOTS1) {
+        const int q4 = s % (G::TX / 4);
+        const int rr = (s / (G::TX / 4)) % G::TY;
+        const int cc = s / ((G::TX / 4) * G::TY);
+        float* row = F1 + (cc * G::TY + rr) * G::RS1;
+        const float e[4] = {r1[it].x, r1[it].y, r1[it].z, r1[it].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[lds_col<G>(4 * q4 + i)] = e[i];
+      }
+    }
+  }
+};
+
+template <class G, typename T>
+__global__ __launch_bounds__(G::THREADS) void corr_fwd_tiled(
+    const T* __restrict__ in1, const T* __restrict__ in2, T* __restrict__ out, int B, int C,
+    int H, int W, int Ho, int Wo, int off, int layout, float divisor, int n_ty, int n_tx,
+    int vec_ok_i) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const bool vec_ok = vec_ok_i != 0;
+
+  const int nblk = gridDim.x;
+  const int t = xcd_remap(blockIdx.x, nblk);
+  const int tx_tile = t % n_tx;
+  const int ty_tile = (t / n_tx) % n_ty;
+  const int n = t / (n_tx * n_ty);
+  const int oy0 = ty_tile * G::TY, ox0 = tx_tile * G::TX;
+  const int y1 = oy0 + off, x1 = ox0 + off;  // f1 tile origin (unpadded image coordinates)
+
+  // thread role
+  const int g = threadIdx.x % G::NG;
+  const int ty = (threadIdx.x / G::NG) % G::TY;
+  const int tjx = threadIdx.x / (G::NG * G::TY);  // 0 .. D-1, wave-uniform when NG*TY % 64 == 0
+  const int p = g % G::GS;
+  const int q = g / G::GS;
+
+  const size_t plane = (size_t)H * W;
+  const T* f1n = in1 + (size_t)n * C * plane;
+  const T* f2n = in2 + (size_t)n * C * plane;
+
+  float acc[G::D][G::PX];
+#pragma unroll
+  for (int a = 0; a < G::D; ++a)
+#pragma unroll
+    for (int k = 0; k < G::PX; ++k) acc[a][k] = 0.f;
+
+  Stager<G, T> st;
+  const int nchunks = (C + G::CC - 1) / G::CC;
+  st.load(f1n, f2n, 0, C, H, W, y1, x1, vec_ok);
+  st.store(lds);
+  __syncthreads();
+
+  // lane-constant LDS offsets
+  const int f2_row = ty + tjx * G::S;  // f2 tile row of this thread's displacement row
+  const int f2_off = f2_row * G::RS2 + (q * G::GS + p) * 4;  // first quad of the window
+  const int f1_off = ty * G::RS1 + (q * G::GS + p) * 4;
+
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const float* buf = lds + (ch & 1) * G::BUF_FLOATS;
+    if (ch + 1 < nchunks) st.load(f1n, f2n, (ch + 1) * G::CC, C, H, W, y1, x1, vec_ok);
+#pragma unroll
+    for (int cc = 0; cc < G::CC; ++cc) {
+      const float* F2 = buf + cc * G::R2 * G::RS2 + f2_off;
+      const float* F1 = buf + G::F2_FLOATS + cc * G::TY * G::RS1 + f1_off;
+      const float4 a4 = *reinterpret_cast<const float4*>(F1);
+      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+      float w[G::NW];
+#pragma unroll
+      for (int u = 0; u < G::NW / 4; ++u) {
+        const float4 b4 = *reinterpret_cast<const float4*>(F2 + u * 4 * G::GS);
+        w[4 * u + 0] = b4.x;
+        w[4 * u + 1] = b4.y;
+        w[4 * u + 2] = b4.z;
+        w[4 * u + 3] = b4.w;
+      }
+#pragma unroll
+      for (int ti = 0; ti < G::D; ++ti)
+#pragma unroll
+        for (int k = 0; k < G::PX; ++k) {
+          const int j = (G::GS == G::S) ? (k + ti) : (k + G::S * ti);
+          acc[ti][k] = fmaf(av[k], w[j], acc[ti][k]);
+        }
+    }
+    if (ch + 1 < nchunks) st.store(lds + ((ch + 1) & 1) * G::BUF_FLOATS);
+    __syncthreads();
+  }
+
+  // epilogue: out[n][ch][oy][ox] = acc / divisor  (cu:100 divides by k*k*C)
+  const int oy = oy0 + ty;
+  if (oy >= Ho) return;
+  const int OC = G::D * G::D;
+  const int tj = tjx - G::DR;
+#pragma unroll
+  for (int ti = 0; ti < G::D; ++ti) {
+    const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
+    T* orow = out + (((size_t)n * OC + oc) * Ho + oy) * Wo;
+    if constexpr (G::GS == 1) {
+      const int ox = ox0 + q * G::PX;
+      if (sizeof(T) == 4 && vec_ok && ox + 3 < Wo) {
+        float4 v = make_float4(acc[ti][0] / divisor, acc[ti][1] / divisor,
+                               acc[ti][2] / divisor, acc[ti][3] / divisor);
+        *reinterpret_cast<float4*>(orow + ox) = v;
+        continue;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < G::PX; ++k) {
+      const int ox = ox0 + q * G::GS * G::PX + p + G::GS * k;
+      if (ox < Wo) orow[ox] = from_f32<T>(acc[ti][k] / divisor);
+    }
+  }
+}
+
+// Generic kernel: one thread per output element, literal cu:34-106 arithmetic.
+template <typename T>
+__global__ void corr_fwd_generic(const T* __restrict__ in1, const T* __restrict__ in2,
+                                 T* __restrict__ out, int B, int C, int H, int W, int Ho,
+                                 int Wo, int pad, int kr, int md, int s1, int s2, int dr,
+                                 int layout, float divisor) {
+  const int D = 2 * dr + 1, OC = D * D;
+  const size_t total = (size_t)B * OC * Ho * Wo;
+  const size_t plane = (size_t)H * W;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int ox = idx % Wo;
+    const int oy = (idx / Wo) % Ho;
+    const int tc = (idx / ((size_t)Wo * Ho)) % OC;
+    const int n = idx / ((size_t)Wo * Ho * OC);
+    const int tj = tc / D - dr, ti = tc % D - dr;
+    const int y1 = oy * s1 + md + kr - pad, x1 = ox * s1 + md + kr - pad;  // unpadded
+    const int y2 = y1 + tj * s2, x2 = x1 + ti * s2;
+    float sum = 0.f;
+    for (int j = -kr; j <= kr; ++j)
+      for (int i = -kr; i <= kr; ++i) {
+        const int ya = y1 + j, xa = x1 + i, yb = y2 + j, xb = x2 + i;
+        if (ya < 0 || ya >= H || xa < 0 || xa >= W || yb < 0 || yb >= H || xb < 0 || xb >= W)
+          continue;
+        const T* pa = in1 + (size_t)n * C * plane + (size_t)ya * W + xa;
+        const T* pb = in2 + (size_t)n * C * plane + (size_t)yb * W + xb;
+        for (int c = 0; c < C; ++c) sum = fmaf(to_f32(pa[c * plane]), to_f32(pb[c * plane]), sum);
+      }
+    const int oc = layout == kCvl ? cvl_channel(tj * s2, ti * s2, dr) : tc;
+    out[(((size_t)n * OC + oc) * Ho + oy) * Wo + ox] = from_f32<T>(sum / divisor);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// host-side launchers
+// ------------------------------------------------------------------------------------
+using Corr9 = CorrTile</*DR*/ 4, /*S*/ 2, /*GS*/ 2, /*PX*/ 4, /*NQ*/ 2, /*TY*/ 16, /*CC*/ 4>;
+using Corr4 = CorrTile</*DR*/ 4, /*S*/ 1, /*GS*/ 1, /*PX*/ 4, /*NQ*/ 4, /*TY*/ 16, /*CC*/ 4>;
+
+template <class G, typename T>
+static hipError_t launch_tiled(const void* in1, const void* in2, void* out, int B, int C,
+                               int H, int W, int Ho, int Wo, int off, int layout,
+                               float divisor, hipStream_t stream) {
+  const int n_ty = (Ho + G::TY - 1) / G::TY;
+  const int n_tx = (Wo + G::TX - 1) / G::TX;
+  const long long nblk = (long long)B * n_ty * n_tx;
+  if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+  // float4 loads/stores need 16-B aligned rows and halo-aligned tile origins.
+  const size_t align = 4 * sizeof(T);
+  const bool vec_ok = (W % 4 == 0) && (Wo % 4 == 0) && (off % 4 == 0) && (G::HALO % 4 == 0) &&
+                      ((uintptr_t)in1 % align == 0) && ((uintptr_t)in2 % align == 0) &&
+                      ((uintptr_t)out % 16 == 0);
+  static bool attr_set = false;  // one-time opt-in for > 64 KiB dynamic LDS
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_tiled<G, T>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((corr_fwd_tiled<G, T>), dim3((unsigned)nblk), dim3(G::THREADS),
+                     G::LDS_BYTES, stream, (const T*)in1, (const T*)in2, (T*)out, B, C, H, W,
+                     Ho, Wo, off, layout, divisor, n_ty, n_tx, vec_ok ? 1 : 0);
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_generic(const void* in1, const void* in2, void* out, int B, int C,
+                                 int H, int W, int Ho, int Wo, int pad, int kr, int md, int s1,
+                                 int s2, int dr, int layout, float divisor,
+                                 hipStream_t stream) {
+  const int D = 2 * dr + 1;
+  const size_t total = (size_t)B * D * D * Ho * Wo;
+  if (total == 0) return hipSuccess;
+  const int threads = 256;
+  size_t blocks = (total + threads - 1) / threads;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(corr_fwd_generic<T>, dim3((unsigned)blocks), dim3(threads), 0, stream,
+                     (const T*)in1, (const T*)in2, (T*)out, B, C, H, W, Ho, Wo, pad, kr, md,
+                     s1, s2, dr, layout, divisor);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, int C, int H,
+                          int W, int Ho, int Wo, int pad, int k, int md, int s1, int s2,
+                          int layout, float divisor, hipStream_t stream, int force_generic) {
+  const int kr = (k - 1) / 2;
+  const int dr = md / s2;
+  if (!force_generic && k == 1 && s1 == 1 && dr == 4) {
+    const int off = md - pad;
+    if (s2 == 2)
+      return launch_tiled<Corr9, T>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor,
+                                    stream);
+    if (s2 == 1)
+      return launch_tiled<Corr4, T>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor,
+                                    stream);
+  }
+  return launch_generic<T>(in1, in2, out, B, C, H, W, Ho, Wo, pad, kr, md, s1, s2, dr, layout,
+                           divisor, stream);
+}
+
+template hipError_t corr_forward_t<float>(const void*, const void*, void*, int, int, int, int,
+                                          int, int, int, int, int, int, int, int, float,
+                                          hipStream_t, int);
+template hipError_t corr_forward_t<__half>(const void*, const void*, void*, int, int, int, int,
+                                           int, int, int, int, int, int, int, int, float,
+                                           hipStream_t, int);
+template hipError_t corr_forward_t<__hip_bfloat16>(const void*, const void*, void*, int, int,
+                                                   int, int, int, int, int, int, int, int, int,
+                                                   int, float, hipStream_t, int);
+
+}  // namespace pwc

@@ -1,0 +1,68 @@
+// pwc_common.cuh — shared device helpers for the gfx950 hot-path kernels.
+#pragma once
+
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace pwc {
+
+// ---- element conversion (fp32 accumulate for every storage type) ----
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(__half v) { return __half2float(v); }
+__device__ __forceinline__ float to_f32(__hip_bfloat16 v) { return __bfloat162float(v); }
+
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ __half from_f32<__half>(float v) { return __float2half(v); }
+template <> __device__ __forceinline__ __hip_bfloat16 from_f32<__hip_bfloat16>(float v) {
+  return __float2bfloat16(v);
+}
+
+// Correlation channel layouts.
+//   RASTER: correlation_cuda_kernel.cu:98  tc = (tj+dr)*D + (ti+dr)
+//   CVL:    modules.py:58-72 CostVolumeLayer order, displacement (dy,dx) = (tj*s2, ti*s2)
+enum Layout : int { kRaster = 0, kCvl = 1 };
+
+// CostVolumeLayer channel of displacement (dy, dx) for search range sr (modules.py:58-72):
+// 0 -> (0,0); for i = 1..sr the block of 4+4*sr channels starting at 1+(i-1)*(4+4sr) holds
+// (-i,0),(+i,0),(0,-i),(0,+i) then for j = 1..sr (-i,-j),(+i,+j),(-i,+j),(+i,-j).
+// Note (dy, dx) = (0, ±i) belongs to the block of i = |dx|, and (±i, ±j) to block i = |dy|.
+__host__ __device__ __forceinline__ int cvl_channel(int dy, int dx, int sr) {
+  if (dy == 0 && dx == 0) return 0;
+  if (dx == 0) {
+    int i = dy < 0 ? -dy : dy;
+    return 1 + (i - 1) * (4 + 4 * sr) + (dy < 0 ? 0 : 1);
+  }
+  if (dy == 0) {
+    int i = dx < 0 ? -dx : dx;
+    return 1 + (i - 1) * (4 + 4 * sr) + (dx < 0 ? 2 : 3);
+  }
+  int i = dy < 0 ? -dy : dy;
+  int j = dx < 0 ? -dx : dx;
+  int base = 1 + (i - 1) * (4 + 4 * sr) + 4 + (j - 1) * 4;
+  if (dy < 0 && dx < 0) return base + 0;
+  if (dy > 0 && dx > 0) return base + 1;
+  if (dy < 0) return base + 2;  // (-i, +j)
+  return base + 3;              // (+i, -j)
+}
+
+__host__ __device__ __forceinline__ int out_channel(int layout, int tj, int ti, int dr, int D,
+                                                    int s2) {
+  return layout == kCvl ? cvl_channel(tj * s2, ti * s2, dr)
+                        : (tj + dr) * D + (ti + dr);
+}
+
+// XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle must
+// be bijective"): consecutive logical tiles land on the same XCD (and L2), so neighbouring
+// tiles that re-read each other's halo rows hit the same L2.  Pure speed choice.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = orig % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / 8;
+}
+
+}  // namespace pwc

@@ -1,0 +1,86 @@
+"""ctypes binding of the C ABI in include/pwc_hotpath.h (libpwc_hotpath.so, gfx950).
+
+The library is built in-tree (``make -C pwc-net_pytorch_amd/csrc`` or
+``__graft_entry__.build()``).  There is no CPU fallback: if the library is missing or a
+tensor is not on a HIP device every entry point raises.  ctypes releases the GIL around each
+call, as the reference's cffi wrapper did (correlation_package/_ext/correlation/__init__.py).
+
+``torch`` is imported first so that the HIP runtime torch ships is the one that satisfies the
+library's ``libamdhip64.so.7`` dependency (one runtime per process; torch's streams are then
+valid handles for the library).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libpwc_hotpath.so")
+
+DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+
+# Every symbol the header declares: (name, restype, argtypes).
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_IP = ctypes.POINTER(ctypes.c_int)
+SYMBOLS = {
+    "pwc_abi_version": (_I, []),
+    "pwc_last_error": (ctypes.c_char_p, []),
+    "pwc_corr_output_shape": (_I, [_I] * 7 + [_IP] * 3),
+    "pwc_corr_forward": (_I, [_P, _P, _P] + [_I] * 11 + [_P]),
+    "pwc_corr_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 11 + [_P]),
+    "pwc_cost_volume_forward": (_I, [_P, _P, _P] + [_I] * 6 + [_P]),
+    "pwc_cost_volume_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 6 + [_P]),
+    "pwc_warp_forward": (_I, [_P, _P, _P] + [_I] * 5 + [_P]),
+    "pwc_warp_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 5 + [_P]),
+}
+ABI_VERSION = 1
+
+_lock = threading.Lock()
+_lib = None
+
+
+class HipLibraryMissing(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the hot-path library; raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise HipLibraryMissing(
+                f"pwcnet_amd: HIP library not built ({LIB_PATH}); run "
+                "`make -C pwc-net_pytorch_amd/csrc` or `python -c 'import __graft_entry__ as g; "
+                "g.build()'`")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SYMBOLS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.pwc_abi_version()
+        if v != ABI_VERSION:
+            raise HipLibraryMissing(f"pwcnet_amd: ABI version {v} != expected {ABI_VERSION}")
+        _lib = lib
+    return _lib
+
+
+def check(ret: int, what: str) -> None:
+    """Reference: a 0 return became THError("aborting") (correlation_cuda.c:86-89)."""
+    if ret != 1:
+        msg = load().pwc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} aborting: {msg}")
+
+
+def corr_output_shape(H, W, pad, k, md, s1, s2):
+    oc, oh, ow = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(load().pwc_corr_output_shape(H, W, pad, k, md, s1, s2, ctypes.byref(oc),
+                                       ctypes.byref(oh), ctypes.byref(ow)),
+          "Correlation")
+    return oc.value, oh.value, ow.value

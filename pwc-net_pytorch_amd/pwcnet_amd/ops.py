@@ -1,0 +1,228 @@
+"""Raw device ops over the C ABI plus their autograd Functions.
+
+Each op takes contiguous NCHW tensors on a HIP device (fp32, fp16 or bf16 storage, fp32
+arithmetic), allocates its outputs through the PyTorch caching allocator (caller-owned, as the
+reference's ``input1.new()`` outputs, correlation_package/functions/correlation.py:28-30) and
+enqueues the kernels on the current stream of the tensors' device.  Nothing synchronises.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+
+
+def _ptr(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(dev: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _check_inputs(what: str, *ts: torch.Tensor, dtypes=tuple(_lib.DTYPE_CODES)) -> None:
+    dev = ts[0].device
+    for t in ts:
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{what}: expected tensors, got {type(t)}")
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                f"{what}: pwcnet_amd runs on HIP devices only (got a {t.device} tensor); "
+                "there is no CPU implementation (the reference's correlation.c is a stub too)")
+        if t.device != dev:
+            raise RuntimeError(f"{what}: tensors on different devices ({t.device} vs {dev})")
+        if t.dtype not in dtypes:
+            raise TypeError(f"{what}: unsupported dtype {t.dtype}")
+        if t.dtype != ts[0].dtype:
+            raise TypeError(f"{what}: mixed dtypes {t.dtype} vs {ts[0].dtype}")
+        if t.dim() != 4:
+            raise ValueError(f"{what}: expected NCHW 4-d tensors, got shape {tuple(t.shape)}")
+
+
+def _i32(*vals) -> None:
+    for v in vals:
+        if not (-(2 ** 31) <= int(v) < 2 ** 31):
+            raise ValueError(f"argument {v} does not fit the C ABI's int")
+
+
+# ---------------------------------------------------------------------------------------
+# correlation (correlation_package, cu:34-290)
+# ---------------------------------------------------------------------------------------
+def corr_forward(input1, input2, pad_size, kernel_size, max_displacement, stride1, stride2,
+                 corr_multiply=1):
+    _check_inputs("Correlation", input1, input2)
+    if input1.shape != input2.shape:
+        raise ValueError(f"Correlation: input shapes differ {tuple(input1.shape)} vs "
+                         f"{tuple(input2.shape)}")
+    B, C, H, W = input1.shape
+    _i32(B, C, H, W, input1.numel())
+    OC, Ho, Wo = _lib.corr_output_shape(H, W, pad_size, kernel_size, max_displacement, stride1,
+                                        stride2)
+    out = torch.empty((B, OC, Ho, Wo), dtype=input1.dtype, device=input1.device)
+    if out.numel() == 0:
+        return out
+    _lib.check(_lib.load().pwc_corr_forward(
+        _ptr(input1), _ptr(input2), _ptr(out), B, C, H, W, pad_size, kernel_size,
+        max_displacement, stride1, stride2, corr_multiply, _lib.DTYPE_CODES[input1.dtype],
+        _stream(input1.device)), "Correlation_forward")
+    return out
+
+
+def corr_backward(input1, input2, grad_output, pad_size, kernel_size, max_displacement, stride1,
+                  stride2, corr_multiply=1):
+    _check_inputs("Correlation backward", input1, input2, grad_output)
+    B, C, H, W = input1.shape
+    OC, Ho, Wo = _lib.corr_output_shape(H, W, pad_size, kernel_size, max_displacement, stride1,
+                                        stride2)
+    if tuple(grad_output.shape) != (B, OC, Ho, Wo):
+        raise ValueError(f"Correlation backward: grad_output shape {tuple(grad_output.shape)} "
+                         f"!= {(B, OC, Ho, Wo)}")
+    grad_output = grad_output.contiguous()
+    g1 = torch.empty_like(input1)
+    g2 = torch.empty_like(input2)
+    if g1.numel() == 0:
+        return g1, g2
+    _lib.check(_lib.load().pwc_corr_backward(
+        _ptr(input1), _ptr(input2), _ptr(grad_output), _ptr(g1), _ptr(g2), B, C, H, W,
+        pad_size, kernel_size, max_displacement, stride1, stride2, corr_multiply,
+        _lib.DTYPE_CODES[input1.dtype], _stream(input1.device)), "Correlation_backward")
+    return g1, g2
+
+
+class CorrelationFunction(Function):
+    """Drop-in for correlation_package/functions/correlation.py:7-56 (same signature and
+    defaults, same contiguity asserts, backward returns (g1, g2) + (None,) * 6)."""
+
+    @staticmethod
+    def forward(ctx, input1, input2, pad_size=3, kernel_size=3, max_displacement=20, stride1=1,
+                stride2=2, corr_multiply=1):
+        assert input1.is_contiguous()
+        assert input2.is_contiguous()
+        ctx.save_for_backward(input1, input2)
+        ctx.pad_size = pad_size
+        ctx.kernel_size = kernel_size
+        ctx.max_displacement = max_displacement
+        ctx.stride1 = stride1
+        ctx.stride2 = stride2
+        ctx.corr_multiply = corr_multiply
+        with torch.cuda.device(input1.device) if input1.is_cuda else _nullctx():
+            return corr_forward(input1, input2, pad_size, kernel_size, max_displacement,
+                                stride1, stride2, corr_multiply)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input1, input2 = ctx.saved_tensors
+        with torch.cuda.device(input1.device):
+            g1, g2 = corr_backward(input1, input2, grad_output, ctx.pad_size, ctx.kernel_size,
+                                   ctx.max_displacement, ctx.stride1, ctx.stride2,
+                                   ctx.corr_multiply)
+        return (g1, g2) + (None,) * 6
+
+
+# ---------------------------------------------------------------------------------------
+# CostVolumeLayer (modules.py:45-74)
+# ---------------------------------------------------------------------------------------
+def cost_volume_forward(src, tgt, search_range):
+    _check_inputs("CostVolumeLayer", src, tgt)
+    if src.shape != tgt.shape:
+        raise ValueError("CostVolumeLayer: src/tgt shapes differ")
+    src, tgt = src.contiguous(), tgt.contiguous()
+    B, C, H, W = src.shape
+    K = (2 * search_range + 1) ** 2
+    out = torch.empty((B, K, H, W), dtype=src.dtype, device=src.device)
+    if out.numel() == 0:
+        return out
+    _lib.check(_lib.load().pwc_cost_volume_forward(
+        _ptr(src), _ptr(tgt), _ptr(out), B, C, H, W, search_range, _lib.DTYPE_CODES[src.dtype],
+        _stream(src.device)), "CostVolumeLayer_forward")
+    return out
+
+
+def cost_volume_backward(src, tgt, grad_output, search_range):
+    _check_inputs("CostVolumeLayer backward", src, tgt, grad_output)
+    B, C, H, W = src.shape
+    grad_output = grad_output.contiguous()
+    gs = torch.empty_like(src)
+    gt = torch.empty_like(tgt)
+    if gs.numel() == 0:
+        return gs, gt
+    _lib.check(_lib.load().pwc_cost_volume_backward(
+        _ptr(src), _ptr(tgt), _ptr(grad_output), _ptr(gs), _ptr(gt), B, C, H, W, search_range,
+        _lib.DTYPE_CODES[src.dtype], _stream(src.device)), "CostVolumeLayer_backward")
+    return gs, gt
+
+
+class CostVolumeFunction(Function):
+    @staticmethod
+    def forward(ctx, src, tgt, search_range):
+        src, tgt = src.contiguous(), tgt.contiguous()
+        ctx.save_for_backward(src, tgt)
+        ctx.search_range = search_range
+        with torch.cuda.device(src.device) if src.is_cuda else _nullctx():
+            return cost_volume_forward(src, tgt, search_range)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        src, tgt = ctx.saved_tensors
+        with torch.cuda.device(src.device):
+            gs, gt = cost_volume_backward(src, tgt, grad_output, ctx.search_range)
+        return gs, gt, None
+
+
+# ---------------------------------------------------------------------------------------
+# WarpingLayer (modules.py:25-42)
+# ---------------------------------------------------------------------------------------
+def warp_forward(x, flow):
+    _check_inputs("WarpingLayer", x, flow)
+    B, C, H, W = x.shape
+    if tuple(flow.shape) != (B, 2, H, W):
+        raise ValueError(f"WarpingLayer: flow shape {tuple(flow.shape)} != {(B, 2, H, W)}")
+    x, flow = x.contiguous(), flow.contiguous()
+    out = torch.empty_like(x)
+    if out.numel() == 0:
+        return out
+    _lib.check(_lib.load().pwc_warp_forward(_ptr(x), _ptr(flow), _ptr(out), B, C, H, W,
+                                            _lib.DTYPE_CODES[x.dtype], _stream(x.device)),
+               "WarpingLayer_forward")
+    return out
+
+
+def warp_backward(x, flow, grad_output):
+    _check_inputs("WarpingLayer backward", x, flow, grad_output, dtypes=(torch.float32,))
+    B, C, H, W = x.shape
+    grad_output = grad_output.contiguous()
+    gx = torch.empty_like(x)
+    gf = torch.empty_like(flow)
+    if gf.numel() == 0:
+        return gx, gf
+    _lib.check(_lib.load().pwc_warp_backward(_ptr(x), _ptr(flow), _ptr(grad_output), _ptr(gx),
+                                             _ptr(gf), B, C, H, W, 0, _stream(x.device)),
+               "WarpingLayer_backward")
+    return gx, gf
+
+
+class WarpFunction(Function):
+    @staticmethod
+    def forward(ctx, x, flow):
+        x, flow = x.contiguous(), flow.contiguous()
+        ctx.save_for_backward(x, flow)
+        with torch.cuda.device(x.device) if x.is_cuda else _nullctx():
+            return warp_forward(x, flow)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        x, flow = ctx.saved_tensors
+        with torch.cuda.device(x.device):
+            gx, gf = warp_backward(x, flow, grad_output)
+        return gx, gf
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False

@@ -1,0 +1,130 @@
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, and its host-side
+argument checks behave (no GPU compute is issued by any call here)."""
+import ctypes
+import glob
+import os
+import re
+import types
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+
+def _declared_symbols():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"PWC_API\s+[\w\s\*]+?\b(pwc_\w+)\s*\(", src))
+    return names
+
+
+def test_header_declares_expected_api():
+    names = _declared_symbols()
+    assert {"pwc_corr_forward", "pwc_corr_backward", "pwc_warp_forward", "pwc_warp_backward",
+            "pwc_cost_volume_forward", "pwc_cost_volume_backward", "pwc_corr_output_shape",
+            "pwc_last_error", "pwc_abi_version"} <= names
+
+
+def test_library_exports_every_declared_symbol():
+    from pwcnet_amd import _lib
+    lib = _lib.load()
+    for name in _declared_symbols():
+        assert hasattr(lib, name), name
+        assert name in _lib.SYMBOLS, f"{name} not typed in _lib.SYMBOLS"
+    assert lib.pwc_abi_version() == _lib.ABI_VERSION
+
+
+def test_library_is_gfx950_code_object():
+    from pwcnet_amd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_output_shape_matches_reference_shape_math():
+    from oracle import oracle as O
+    from pwcnet_amd import _lib
+    for args in [(96, 112, 9, 1, 9, 1, 2), (96, 112, 4, 1, 4, 1, 1), (20, 30, 0, 1, 4, 1, 1),
+                 (20, 30, 3, 3, 2, 2, 1), (21, 31, 3, 3, 2, 2, 1), (1, 1, 9, 1, 9, 1, 2),
+                 (384, 448, 20, 1, 20, 1, 2)]:
+        assert _lib.corr_output_shape(*args) == O.corr_output_shape(*args)
+
+
+def test_error_paths_return_zero_with_message():
+    from pwcnet_amd import _lib
+    lib = _lib.load()
+    null = ctypes.c_void_p(0)
+    one = ctypes.c_void_p(16)
+    # unsupported dtype: rejected before any HIP call
+    assert lib.pwc_corr_forward(one, one, one, 1, 1, 4, 4, 9, 1, 9, 1, 2, 1, 7, null) == 0
+    assert b"dtype" in lib.pwc_last_error()
+    # null buffers
+    assert lib.pwc_warp_forward(null, null, null, 1, 1, 4, 4, 0, null) == 0
+    assert b"null" in lib.pwc_last_error()
+    # reference backward is undefined for stride1 != 1
+    assert lib.pwc_corr_backward(one, one, one, one, one, 1, 1, 8, 8, 4, 1, 4, 2, 1, 1, 0,
+                                 null) == 0
+    assert b"stride1" in lib.pwc_last_error()
+    # empty output (pad too small for the displacement)
+    assert lib.pwc_corr_forward(one, one, one, 1, 1, 4, 4, 0, 1, 9, 1, 2, 1, 0, null) == 0
+    assert b"empty" in lib.pwc_last_error()
+    # warp backward is fp32 only
+    assert lib.pwc_warp_backward(one, one, one, one, one, 1, 1, 4, 4, 1, null) == 0
+    with pytest.raises(RuntimeError, match="aborting"):
+        _lib.check(0, "x")
+
+
+def test_layers_fail_loudly_on_cpu_tensors():
+    """No CPU fallback: the product path refuses host tensors."""
+    import pwcnet_amd
+    x = torch.zeros(1, 4, 8, 8)
+    f = torch.zeros(1, 2, 8, 8)
+    with pytest.raises(RuntimeError, match="HIP"):
+        pwcnet_amd.Correlation(9, 1, 9, 1, 2)(x, x)
+    with pytest.raises(RuntimeError, match="HIP"):
+        pwcnet_amd.WarpingLayer(None)(x, f)
+    with pytest.raises(RuntimeError, match="HIP"):
+        pwcnet_amd.CostVolumeLayer(types.SimpleNamespace(search_range=4))(x, x)
+
+
+def test_correlation_module_signature_matches_reference():
+    import inspect
+    from correlation_package.modules.correlation import Correlation
+    from correlation_package.functions.correlation import CorrelationFunction
+    sig = inspect.signature(Correlation.__init__)
+    assert [p for p in sig.parameters][1:] == ["pad_size", "kernel_size", "max_displacement",
+                                                "stride1", "stride2", "corr_multiply"]
+    assert [sig.parameters[p].default for p in list(sig.parameters)[1:]] == [0, 0, 0, 1, 2, 1]
+    fsig = inspect.signature(CorrelationFunction.forward)
+    assert [fsig.parameters[p].default for p in list(fsig.parameters)[3:]] == [3, 3, 20, 1, 2, 1]
+    c = Correlation(pad_size=9, kernel_size=1, max_displacement=9, stride1=1, stride2=2)
+    assert len(list(c.parameters())) == 0 and len(list(c.buffers())) == 0
+
+
+def test_cvl_channel_formula_matches_reference_order():
+    """csrc/pwc_common.cuh cvl_channel() restated in Python vs the oracle's modules.py order."""
+    from oracle import oracle as O
+
+    def cvl_channel(dy, dx, sr):
+        if dy == 0 and dx == 0:
+            return 0
+        if dx == 0:
+            i = abs(dy)
+            return 1 + (i - 1) * (4 + 4 * sr) + (0 if dy < 0 else 1)
+        if dy == 0:
+            i = abs(dx)
+            return 1 + (i - 1) * (4 + 4 * sr) + (2 if dx < 0 else 3)
+        i, j = abs(dy), abs(dx)
+        base = 1 + (i - 1) * (4 + 4 * sr) + 4 + (j - 1) * 4
+        if dy < 0 and dx < 0:
+            return base
+        if dy > 0 and dx > 0:
+            return base + 1
+        return base + 2 if dy < 0 else base + 3
+
+    for sr in (1, 2, 3, 4, 8):
+        dys, dxs = O.cvl_offsets(sr)
+        for k, (dy, dx) in enumerate(zip(dys, dxs)):
+            assert cvl_channel(dy, dx, sr) == k, (sr, dy, dx, k)

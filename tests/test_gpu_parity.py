@@ -1,0 +1,244 @@
+"""GPU parity: the HIP hot path (through the C ABI) against the CPU oracle and the reference's
+golden fixtures.
+
+Tolerances (BASELINE.json north_star: "within 1e-5 fp32"):
+  * fp32 forward: |hip - oracle_f64| <= 1e-5 + 1e-5*|oracle| on unit-scale inputs
+  * fp32 backward: 1e-4
+  * fp16/bf16 storage: compared with the fp64 oracle on the *rounded* inputs; tolerance is the
+    output rounding of the storage type (fp16 2e-3 rel, bf16 1.6e-2 rel) + 1e-4 abs.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+CORR_CASES = [
+    # (B, C, H, W, pad, k, md, s1, s2)  -- tiled kernels: k=1, s1=1, md/s2 == 4
+    (2, 8, 12, 14, 9, 1, 9, 1, 2),      # Corr9 (model.py:24), tiny
+    (2, 32, 24, 28, 9, 1, 9, 1, 2),
+    (1, 192, 6, 7, 9, 1, 9, 1, 2),      # l0 shape at 384x448
+    (1, 128, 12, 14, 9, 1, 9, 1, 2),    # l1
+    (1, 96, 24, 28, 9, 1, 9, 1, 2),     # l2
+    (1, 64, 48, 56, 9, 1, 9, 1, 2),     # l3
+    (2, 32, 96, 112, 9, 1, 9, 1, 2),    # l4
+    (1, 3, 17, 23, 9, 1, 9, 1, 2),      # ragged: W % 4 != 0, C % CC != 0
+    (1, 5, 1, 1, 9, 1, 9, 1, 2),        # 1x1 image
+    (2, 8, 12, 14, 4, 1, 4, 1, 1),      # Corr4
+    (2, 32, 24, 28, 4, 1, 4, 1, 1),
+    (1, 7, 19, 13, 4, 1, 4, 1, 1),      # ragged Corr4
+    (1, 16, 20, 24, 0, 1, 4, 1, 1),     # pad < md: off = 4 (vector loads disabled), Ho=H-8
+    (1, 16, 20, 24, 8, 1, 8, 1, 2),     # md=8, s2=2 -> dr=4, tiled with off=0
+    (1, 16, 20, 24, 6, 1, 9, 1, 2),     # off = 3: misaligned tile origin
+    # generic kernel
+    (2, 8, 12, 14, 3, 3, 2, 1, 1),      # kernel_size 3
+    (2, 8, 13, 15, 4, 1, 4, 2, 2),      # stride1 2
+    (1, 8, 12, 14, 2, 1, 2, 1, 1),      # dr = 2
+    (1, 8, 12, 14, 20, 1, 20, 1, 2),    # FlowNetC-style md=20, s2=2 (dr=10)
+]
+
+
+def _t(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def _rand(rng, *shape):
+    return rng.standard_normal(shape).astype(np.float32)
+
+
+@pytest.mark.parametrize("case", CORR_CASES, ids=lambda c: "B{}C{}_{}x{}_p{}k{}md{}s{}{}".format(*c))
+def test_corr_forward_fp32(case):
+    from pwcnet_amd.ops import corr_forward
+    B, C, H, W, pad, k, md, s1, s2 = case
+    rng = np.random.default_rng(hash(case) % 2**32)
+    a, b = _rand(rng, B, C, H, W), _rand(rng, B, C, H, W)
+    out = corr_forward(_t(a), _t(b), pad, k, md, s1, s2)
+    torch.cuda.synchronize()
+    ref = O.corr_forward(a, b, pad, k, md, s1, s2)
+    assert tuple(out.shape) == ref.shape
+    np.testing.assert_allclose(_np(out), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("case", [c for c in CORR_CASES if c[7] == 1],
+                         ids=lambda c: "B{}C{}_{}x{}_p{}k{}md{}s{}{}".format(*c))
+def test_corr_backward_fp32(case):
+    from pwcnet_amd.ops import corr_backward
+    B, C, H, W, pad, k, md, s1, s2 = case
+    rng = np.random.default_rng(1 + hash(case) % 2**31)
+    a, b = _rand(rng, B, C, H, W), _rand(rng, B, C, H, W)
+    OC, Ho, Wo = O.corr_output_shape(H, W, pad, k, md, s1, s2)
+    g = _rand(rng, B, OC, Ho, Wo)
+    g1, g2 = corr_backward(_t(a), _t(b), _t(g), pad, k, md, s1, s2)
+    torch.cuda.synchronize()
+    r1, r2 = O.corr_backward(a, b, g, pad, k, md, s1, s2)
+    np.testing.assert_allclose(_np(g1), r1, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(g2), r2, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype,rtol", [(torch.float16, 2e-3), (torch.bfloat16, 1.6e-2)])
+@pytest.mark.parametrize("case", [(2, 32, 24, 28, 9, 1, 9, 1, 2), (1, 16, 17, 23, 4, 1, 4, 1, 1),
+                                  (1, 8, 12, 14, 3, 3, 2, 1, 1)])
+def test_corr_forward_low_precision(case, dtype, rtol):
+    from pwcnet_amd.ops import corr_forward
+    B, C, H, W, pad, k, md, s1, s2 = case
+    rng = np.random.default_rng(7)
+    a, b = _t(_rand(rng, B, C, H, W), dtype), _t(_rand(rng, B, C, H, W), dtype)
+    out = corr_forward(a, b, pad, k, md, s1, s2)
+    assert out.dtype == dtype
+    ref = O.corr_forward(_np(a), _np(b), pad, k, md, s1, s2)
+    np.testing.assert_allclose(_np(out), ref, rtol=rtol, atol=1e-4 + rtol * np.abs(ref).max())
+
+
+def test_correlation_module_autograd_matches_oracle():
+    """Correlation nn.Module + CorrelationFunction end to end (model.py:24 config)."""
+    from correlation_package.modules.correlation import Correlation
+    rng = np.random.default_rng(3)
+    a, b = _rand(rng, 2, 16, 20, 24), _rand(rng, 2, 16, 20, 24)
+    x1 = _t(a).requires_grad_(True)
+    x2 = _t(b).requires_grad_(True)
+    corr = Correlation(pad_size=9, kernel_size=1, max_displacement=9, stride1=1, stride2=2,
+                       corr_multiply=1)
+    out = corr(x1, x2)
+    g = _rand(rng, *out.shape)
+    out.backward(_t(g))
+    np.testing.assert_allclose(_np(out), O.corr_forward(a, b, 9, 1, 9, 1, 2), rtol=1e-5,
+                               atol=1e-5)
+    r1, r2 = O.corr_backward(a, b, g, 9, 1, 9, 1, 2)
+    np.testing.assert_allclose(_np(x1.grad), r1, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(x2.grad), r2, rtol=1e-4, atol=1e-4)
+
+
+def test_correlation_asserts_contiguous():
+    from pwcnet_amd.ops import CorrelationFunction
+    x = torch.randn(1, 8, 12, 14, device=DEV).transpose(2, 3)
+    with pytest.raises(AssertionError):
+        CorrelationFunction.apply(x, x, 9, 1, 9, 1, 2, 1)
+
+
+def test_corr_empty_batch():
+    from pwcnet_amd.ops import corr_forward
+    x = torch.zeros(0, 8, 12, 14, device=DEV)
+    assert tuple(corr_forward(x, x, 9, 1, 9, 1, 2).shape) == (0, 81, 12, 14)
+
+
+# ---------------------------------------------------------------------------------------
+# reference fixtures (outputs of the reference's own modules.py, tests/golden)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "cvl_*.npz"))),
+                         ids=os.path.basename)
+def test_cost_volume_layer_vs_reference(path):
+    import types
+    from pwcnet_amd import CostVolumeLayer
+    z = np.load(path)
+    sr = int(z["sr"])
+    layer = CostVolumeLayer(types.SimpleNamespace(search_range=sr, device=DEV))
+    s = _t(z["src"]).requires_grad_(True)
+    t = _t(z["tgt"]).requires_grad_(True)
+    out = layer(s, t)
+    out.backward(_t(z["gout"]))
+    np.testing.assert_allclose(_np(out), z["out"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_np(s.grad), z["gsrc"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(t.grad), z["gtgt"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "cvl_sr*.npz"))),
+                         ids=os.path.basename)
+def test_correlation_vs_reference_cvl(path):
+    """Correlation (Corr4 / Corr9) against the reference CVL through the channel pin."""
+    from pwcnet_amd.ops import corr_forward
+    z = np.load(path)
+    sr = int(z["sr"])
+    C = z["src"].shape[1]
+    K = (2 * sr + 1) ** 2
+    pad, md, s2 = (4, 4, 1) if sr == 4 else (9, 9, 2)
+    idx = O.corr_channel_from_cvl(sr, s2, md)
+    out = corr_forward(_t(z["src"]), _t(z["tgt"]), pad, 1, md, 1, s2)
+    np.testing.assert_allclose(_np(out) * C, z["out"][:, idx] * K, rtol=1e-5, atol=2e-5 * C)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "warp_*.npz"))),
+                         ids=os.path.basename)
+def test_warping_layer_vs_reference(path):
+    from pwcnet_amd import WarpingLayer
+    z = np.load(path)
+    x = _t(z["x"]).requires_grad_(True)
+    f = _t(z["flow"]).requires_grad_(True)
+    out = WarpingLayer(None)(x, f)
+    out.backward(_t(z["gout"]))
+    np.testing.assert_allclose(_np(out), z["out"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_np(x.grad), z["gx"], rtol=1e-4, atol=1e-4)
+    # same fp32 chain as the reference: even the zero-flow (integer coordinate) case agrees
+    np.testing.assert_allclose(_np(f.grad), z["gflow"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 96, 112), (1, 192, 6, 7), (3, 5, 9, 31),
+                                   (1, 16, 448 // 4, 1024 // 4)])
+def test_warp_vs_oracle(shape):
+    from pwcnet_amd.ops import warp_backward, warp_forward
+    B, C, H, W = shape
+    rng = np.random.default_rng(11)
+    x = _rand(rng, B, C, H, W)
+    f = (rng.standard_normal((B, 2, H, W)) * 3).astype(np.float32)
+    out = warp_forward(_t(x), _t(f))
+    np.testing.assert_allclose(_np(out), O.warp_forward(x, f), rtol=1e-5, atol=1e-5)
+    g = _rand(rng, B, C, H, W)
+    gx, gf = warp_backward(_t(x), _t(f), _t(g))
+    rx, rf = O.warp_backward(x, f, g)
+    np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
+
+
+def test_warp_fp16():
+    from pwcnet_amd.ops import warp_forward
+    rng = np.random.default_rng(5)
+    x = _t(_rand(rng, 2, 16, 24, 28), torch.float16)
+    f = _t(rng.standard_normal((2, 2, 24, 28)) * 3, torch.float16)
+    out = warp_forward(x, f)
+    ref = O.warp_forward(_np(x), _np(f))
+    np.testing.assert_allclose(_np(out), ref, rtol=2e-3, atol=5e-3)
+
+
+# ---------------------------------------------------------------------------------------
+# full BASELINE sizes: size-independent properties + full oracle compare (seconds on CPU)
+# ---------------------------------------------------------------------------------------
+def test_level2_full_size_corr9_b8():
+    """Config 2 l4 ('level 2'): B=8, 32x96x112, Corr9 — full compare with the oracle."""
+    from pwcnet_amd.ops import corr_forward
+    rng = np.random.default_rng(2024)
+    a, b = _rand(rng, 8, 32, 96, 112), _rand(rng, 8, 32, 96, 112)
+    out = _np(corr_forward(_t(a), _t(b), 9, 1, 9, 1, 2))
+    np.testing.assert_allclose(out, O.corr_forward(a, b, 9, 1, 9, 1, 2), rtol=1e-5, atol=1e-5)
+
+
+def test_correlation_properties_sintel_fp16():
+    """Config 4 l4 (B=16, 32x112x256, fp16): symmetry property
+    corr(a, b)[tc] at x == corr(b, a)[mirror tc] at x + d (size-independent check),
+    plus a full oracle compare on two images of the batch."""
+    from pwcnet_amd.ops import corr_forward
+    rng = np.random.default_rng(99)
+    a = _t(_rand(rng, 16, 32, 112, 256), torch.float16)
+    b = _t(_rand(rng, 16, 32, 112, 256), torch.float16)
+    ab = corr_forward(a, b, 9, 1, 9, 1, 2).float()
+    ba = corr_forward(b, a, 9, 1, 9, 1, 2).float()
+    # displacement (dy,dx)=(2,2): channel (tj=1,ti=1) -> 6*9+... raster tc=(1+4)*9+(1+4)=50,
+    # mirror (-1,-1) -> tc=(3)*9+3=30: ab[50][y][x] == ba[30][y+2][x+2]
+    torch.testing.assert_close(ab[:, 50, :-2, :-2], ba[:, 30, 2:, 2:], rtol=0, atol=2e-3)
+    ref = O.corr_forward(_np(a[:2]), _np(b[:2]), 9, 1, 9, 1, 2)
+    np.testing.assert_allclose(_np(ab[:2]), ref, rtol=2e-3, atol=2e-3)
+
+
+def test_layers_reject_cpu_tensors():
+    from pwcnet_amd.ops import corr_forward
+    with pytest.raises(RuntimeError):
+        corr_forward(torch.zeros(1, 2, 3, 3), torch.zeros(1, 2, 3, 3), 9, 1, 9, 1, 2)
