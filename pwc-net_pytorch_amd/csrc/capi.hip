@@ -58,13 +58,16 @@ bool corr_shape(int H, int W, int pad, int k, int md, int s1, int s2, int* oc, i
   return true;
 }
 
-// FORCE_GENERIC (env PWC_FORCE_GENERIC=1) routes correlation to the generic kernels; used by
-// the parity tests to cross-check the tiled kernels against the literal restatement.
+// Kernel-selection override for cross-checks (env PWC_CORR_PATH, read once):
+//   "generic" (1): literal one-thread-per-output kernels only;
+//   "regtile" (2): skip the LDS-DMA ring kernel, use the register-staged tiled kernel.
 int force_generic() {
   static int v = -1;
   if (v < 0) {
-    const char* s = std::getenv("PWC_FORCE_GENERIC");
-    v = (s && s[0] == '1') ? 1 : 0;
+    const char* s = std::getenv("PWC_CORR_PATH");
+    v = 0;
+    if (s && std::strcmp(s, "generic") == 0) v = 1;
+    if (s && std::strcmp(s, "regtile") == 0) v = 2;
   }
   return v;
 }

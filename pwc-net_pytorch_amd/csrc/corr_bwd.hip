@@ -162,7 +162,7 @@ hipError_t corr_backward_t(const void* in1, const void* in2, const void* gout, v
   const int dr = md / s2;
   const size_t npix = (size_t)B * H * W;
   if (npix == 0 || C == 0) return hipSuccess;
-  if (!force_generic && k == 1 && s1 == 1) {
+  if (force_generic != 1 && k == 1 && s1 == 1) {
     constexpr int CB = 8;
     const int off = md - pad;
     dim3 grid((unsigned)((npix + 255) / 256), (unsigned)((C + CB - 1) / CB));

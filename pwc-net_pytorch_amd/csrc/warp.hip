@@ -16,7 +16,10 @@ namespace pwc {
 
 // torch.linspace(-1, 1, n)[i] in fp32 (ATen RangeFactories: step = (end-start)/(n-1),
 // lower half start + step*i, upper half end - step*(n-1-i)).
+// hipcc lowers __fmul_rn/__fadd_rn to plain operators, so contraction is disabled explicitly
+// in the coordinate chain: an fma there would round differently from the reference.
 __device__ __forceinline__ float linspace_m1p1(int i, int n) {
+#pragma clang fp contract(off)
   if (n == 1) return -1.f;
   const float step = __fdiv_rn(2.f, (float)(n - 1));
   return (i < n / 2) ? __fadd_rn(-1.f, __fmul_rn(step, (float)i))
@@ -26,6 +29,7 @@ __device__ __forceinline__ float linspace_m1p1(int i, int n) {
 // Source coordinate of the reference chain for one axis.  `half` = (size-1.0)/2.0 computed in
 // double on the host (Python float), divided in fp32 like tensor / python-float.
 __device__ __forceinline__ float src_coord(float disp, int i, int n, float half) {
+#pragma clang fp contract(off)
   const float g = __fadd_rn(linspace_m1p1(i, n), __fdiv_rn(disp, half));
   return __fmul_rn(__fdiv_rn(__fadd_rn(g, 1.f), 2.f), (float)(n - 1));
 }
@@ -37,6 +41,7 @@ struct Bilinear {
 };
 
 __device__ __forceinline__ Bilinear bilinear(float ix, float iy, int H, int W) {
+#pragma clang fp contract(off)
   Bilinear b;
   const float fx = floorf(ix), fy = floorf(iy);
   b.x0 = (int)fx;
@@ -53,85 +58,129 @@ __device__ __forceinline__ Bilinear bilinear(float ix, float iy, int H, int W) {
   return b;
 }
 
-// One thread per output pixel and CB channels (grid.y splits the channels).
+// Corner addresses clamped into the image plus validity masks: every gather is issued
+// unconditionally (one batch of loads per thread, no per-corner branches), invalid corners are
+// zeroed after the load -- the reference's "skip out-of-bounds corners" (zeros padding).
+struct Corners {
+  unsigned i00, i01, i10, i11;
+  float m00, m01, m10, m11;  // 1 where the corner is inside the image
+};
+
+__device__ __forceinline__ Corners corners(const Bilinear& b, int H, int W) {
+  const int x0 = min(max(b.x0, 0), W - 1), x1 = min(max(b.x0 + 1, 0), W - 1);
+  const int y0 = min(max(b.y0, 0), H - 1), y1 = min(max(b.y0 + 1, 0), H - 1);
+  Corners k;
+  k.i00 = (unsigned)(y0 * W + x0);
+  k.i01 = (unsigned)(y0 * W + x1);
+  k.i10 = (unsigned)(y1 * W + x0);
+  k.i11 = (unsigned)(y1 * W + x1);
+  k.m00 = (b.vy0 && b.vx0) ? 1.f : 0.f;
+  k.m01 = (b.vy0 && b.vx1) ? 1.f : 0.f;
+  k.m10 = (b.vy1 && b.vx0) ? 1.f : 0.f;
+  k.m11 = (b.vy1 && b.vx1) ? 1.f : 0.f;
+  return k;
+}
+
+__device__ __forceinline__ float masked(float v, float m) { return m != 0.f ? v : 0.f; }
+
+// One thread per output pixel and CB channels (grid.y splits the channels).  32-bit indexing
+// (the launcher checks B*C*H*W < 2^31).
 template <typename T, int CB>
 __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ flow,
                                                        T* __restrict__ out, int B, int C, int H,
                                                        int W, float halfx, float halfy) {
-  const size_t plane = (size_t)H * W;
-  const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (idx >= (size_t)B * plane) return;
-  const int px = idx % W;
-  const int py = (idx / W) % H;
-  const int n = idx / plane;
-  const size_t pix = (size_t)py * W + px;
-  const float u = to_f32(flow[((size_t)n * 2 + 0) * plane + pix]);
-  const float v = to_f32(flow[((size_t)n * 2 + 1) * plane + pix]);
+  const unsigned plane = (unsigned)(H * W);
+  const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= (unsigned)B * plane) return;
+  const unsigned n = idx / plane;
+  const unsigned pix = idx - n * plane;
+  const int py = (int)(pix / (unsigned)W);
+  const int px = (int)pix - py * W;
+  const float u = to_f32(flow[(2 * n + 0) * plane + pix]);
+  const float v = to_f32(flow[(2 * n + 1) * plane + pix]);
   const float ix = src_coord(u, px, W, halfx);
   const float iy = src_coord(v, py, H, halfy);
   const Bilinear b = bilinear(ix, iy, H, W);
+  const Corners k = corners(b, H, W);
   const float w00 = __fmul_rn(b.wx0, b.wy0), w01 = __fmul_rn(b.wx1, b.wy0);
   const float w10 = __fmul_rn(b.wx0, b.wy1), w11 = __fmul_rn(b.wx1, b.wy1);
-  const size_t i00 = (size_t)b.y0 * W + b.x0;
   const int c0 = blockIdx.y * CB;
+  float r[CB][4];
 #pragma unroll
   for (int i = 0; i < CB; ++i) {
-    const int c = c0 + i;
-    if (c >= C) break;
-    const T* p = x + ((size_t)n * C + c) * plane;
+    const int c = min(c0 + i, C - 1);
+    const T* p = x + ((unsigned)(n * C + c)) * plane;
+    r[i][0] = to_f32(p[k.i00]);
+    r[i][1] = to_f32(p[k.i01]);
+    r[i][2] = to_f32(p[k.i10]);
+    r[i][3] = to_f32(p[k.i11]);
+  }
+#pragma unroll
+  for (int i = 0; i < CB; ++i) {
     float acc = 0.f;
-    if (b.vy0 && b.vx0) acc = fmaf(to_f32(p[i00]), w00, acc);
-    if (b.vy0 && b.vx1) acc = fmaf(to_f32(p[i00 + 1]), w01, acc);
-    if (b.vy1 && b.vx0) acc = fmaf(to_f32(p[i00 + W]), w10, acc);
-    if (b.vy1 && b.vx1) acc = fmaf(to_f32(p[i00 + W + 1]), w11, acc);
-    out[((size_t)n * C + c) * plane + pix] = from_f32<T>(acc);
+    acc = fmaf(masked(r[i][0], k.m00), w00, acc);
+    acc = fmaf(masked(r[i][1], k.m01), w01, acc);
+    acc = fmaf(masked(r[i][2], k.m10), w10, acc);
+    acc = fmaf(masked(r[i][3], k.m11), w11, acc);
+    if (c0 + i < C) out[((unsigned)(n * C + c0 + i)) * plane + pix] = from_f32<T>(acc);
   }
 }
 
 // fp32 only: grad_x accumulated with atomics (zeroed by the launcher), grad_flow per pixel.
+// Channels are processed CB at a time with all loads of a group issued together.
+template <int CB>
 __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
                                                        const float* __restrict__ gout,
                                                        float* __restrict__ gx,
                                                        float* __restrict__ gflow, int B, int C,
                                                        int H, int W, float halfx, float halfy) {
-  const size_t plane = (size_t)H * W;
-  const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (idx >= (size_t)B * plane) return;
-  const int px = idx % W;
-  const int py = (idx / W) % H;
-  const int n = idx / plane;
-  const size_t pix = (size_t)py * W + px;
-  const float u = flow[((size_t)n * 2 + 0) * plane + pix];
-  const float v = flow[((size_t)n * 2 + 1) * plane + pix];
+  const unsigned plane = (unsigned)(H * W);
+  const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= (unsigned)B * plane) return;
+  const unsigned n = idx / plane;
+  const unsigned pix = idx - n * plane;
+  const int py = (int)(pix / (unsigned)W);
+  const int px = (int)pix - py * W;
+  const float u = flow[(2 * n + 0) * plane + pix];
+  const float v = flow[(2 * n + 1) * plane + pix];
   const float ix = src_coord(u, px, W, halfx);
   const float iy = src_coord(v, py, H, halfy);
   const Bilinear b = bilinear(ix, iy, H, W);
+  const Corners k = corners(b, H, W);
   const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;
   const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
-  const size_t i00 = (size_t)b.y0 * W + b.x0;
   float gix = 0.f, giy = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float* p = x + ((size_t)n * C + c) * plane;
-    float* q = gx + ((size_t)n * C + c) * plane;
-    const float go = gout[((size_t)n * C + c) * plane + pix];
-    const float v00 = (b.vy0 && b.vx0) ? p[i00] : 0.f;
-    const float v01 = (b.vy0 && b.vx1) ? p[i00 + 1] : 0.f;
-    const float v10 = (b.vy1 && b.vx0) ? p[i00 + W] : 0.f;
-    const float v11 = (b.vy1 && b.vx1) ? p[i00 + W + 1] : 0.f;
-    if (b.vy0 && b.vx0) atomicAdd(q + i00, go * w00);
-    if (b.vy0 && b.vx1) atomicAdd(q + i00 + 1, go * w01);
-    if (b.vy1 && b.vx0) atomicAdd(q + i00 + W, go * w10);
-    if (b.vy1 && b.vx1) atomicAdd(q + i00 + W + 1, go * w11);
-    gix += go * ((v01 - v00) * b.wy0 + (v11 - v10) * b.wy1);
-    giy += go * ((v10 - v00) * b.wx0 + (v11 - v01) * b.wx1);
+  for (int c0 = 0; c0 < C; c0 += CB) {
+    float r[CB][4], go[CB];
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = min(c0 + i, C - 1);
+      const float* p = x + ((unsigned)(n * C + c)) * plane;
+      r[i][0] = masked(p[k.i00], k.m00);
+      r[i][1] = masked(p[k.i01], k.m01);
+      r[i][2] = masked(p[k.i10], k.m10);
+      r[i][3] = masked(p[k.i11], k.m11);
+      go[i] = (c0 + i < C) ? gout[((unsigned)(n * C + c)) * plane + pix] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      if (c0 + i >= C) break;
+      float* q = gx + ((unsigned)(n * C + c0 + i)) * plane;
+      if (k.m00 != 0.f) atomicAdd(q + k.i00, go[i] * w00);
+      if (k.m01 != 0.f) atomicAdd(q + k.i01, go[i] * w01);
+      if (k.m10 != 0.f) atomicAdd(q + k.i10, go[i] * w10);
+      if (k.m11 != 0.f) atomicAdd(q + k.i11, go[i] * w11);
+      gix += go[i] * ((r[i][1] - r[i][0]) * b.wy0 + (r[i][3] - r[i][2]) * b.wy1);
+      giy += go[i] * ((r[i][2] - r[i][0]) * b.wx0 + (r[i][3] - r[i][1]) * b.wx1);
+    }
   }
   // grid grad (ATen: * (size-1)/2) then through flow / ((size-1)/2): net factor 1 in exact
   // arithmetic; keep the two fp32 roundings of the reference chain.
   const float mx = (float)(W - 1) / 2.f, my = (float)(H - 1) / 2.f;
-  gflow[((size_t)n * 2 + 0) * plane + pix] = (gix * mx) / halfx;
-  gflow[((size_t)n * 2 + 1) * plane + pix] = (giy * my) / halfy;
+  gflow[(2 * n + 0) * plane + pix] = (gix * mx) / halfx;
+  gflow[(2 * n + 1) * plane + pix] = (giy * my) / halfy;
 }
 
 template <typename T>
@@ -139,6 +188,7 @@ hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int
                           int W, hipStream_t stream) {
   const size_t npix = (size_t)B * H * W;
   if (npix == 0 || C == 0) return hipSuccess;
+  if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
   constexpr int CB = 8;
   const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
   dim3 grid((unsigned)((npix + 255) / 256), (unsigned)((C + CB - 1) / CB));
@@ -151,10 +201,11 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
                              void* gflow, int B, int C, int H, int W, hipStream_t stream) {
   const size_t npix = (size_t)B * H * W;
   if (npix == 0) return hipSuccess;
+  if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(gx, 0, sizeof(float) * npix * C, stream);
   if (e != hipSuccess) return e;
   const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
-  hipLaunchKernelGGL(warp_bwd_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(warp_bwd_kernel<8>, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0,
                      stream, (const float*)x, (const float*)flow, (const float*)gout,
                      (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy);
   return hipGetLastError();

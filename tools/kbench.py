@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Per-kernel timing of the hot path (HIP events, rotating buffers past the Infinity Cache).
+
+    python tools/kbench.py [--batch 8] [--height 384] [--width 448] [--iters 50]
+
+Prints one JSON line per (level, op) with the mean device time and algorithmic GB/s.  The
+kernel path can be forced with PWC_CORR_PATH=generic|regtile (read once per process).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pwc-net_pytorch_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from pwcnet_amd.ops import corr_backward, corr_forward, warp_backward, warp_forward  # noqa
+
+
+def timeit(fn, sets, iters):
+    for s in sets:
+        fn(s)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(iters)]
+    for i, (a, b) in enumerate(evs):
+        s = sets[i % len(sets)]
+        a.record()
+        fn(s)
+        b.record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
+    return ts[len(ts) // 2], sum(ts) / len(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--height", type=int, default=384)
+    ap.add_argument("--width", type=int, default=448)
+    ap.add_argument("--iters", type=int, default=60)
+    ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--backward", action="store_true")
+    args = ap.parse_args()
+    dt = torch.float32 if args.dtype == "fp32" else torch.float16
+    esz = 4 if dt == torch.float32 else 2
+    dev = torch.device("cuda:0")
+    B = args.batch
+    path = os.environ.get("PWC_CORR_PATH", "default")
+    for l, (C, h, w) in enumerate(bench.level_shapes(args.height, args.width)):
+        per = (3 * C * h * w + 83 * h * w) * B * esz
+        n = max(2, int(2 * 256 * 2 ** 20 / per) + 1)
+        g = torch.Generator(device=dev).manual_seed(l)
+        sets = [dict(x1=torch.randn(B, C, h, w, device=dev, generator=g).to(dt),
+                     x2=torch.randn(B, C, h, w, device=dev, generator=g).to(dt),
+                     fl=(torch.randn(B, 2, h, w, device=dev, generator=g) * 2).to(dt))
+                for _ in range(n)]
+        med, mean = timeit(lambda s: corr_forward(s["x1"], s["x2"], 9, 1, 9, 1, 2), sets,
+                           args.iters)
+        cb = bench.corr_bytes_per_pair(C, h, w, esz) * B
+        print(json.dumps(dict(level=l, op="corr_fwd", path=path, shape=[B, C, h, w],
+                              med_us=round(med, 2), mean_us=round(mean, 2),
+                              gbs=round(cb / (med * 1e-6) / 1e9, 1))))
+        med, mean = timeit(lambda s: warp_forward(s["x2"], s["fl"]), sets, args.iters)
+        wb = (2 * C * h * w + 2 * h * w) * B * esz
+        print(json.dumps(dict(level=l, op="warp_fwd", shape=[B, C, h, w], med_us=round(med, 2),
+                              mean_us=round(mean, 2), gbs=round(wb / (med * 1e-6) / 1e9, 1))))
+        if args.backward and dt == torch.float32:
+            go = torch.randn(B, 81, h, w, device=dev)
+            med, mean = timeit(lambda s: corr_backward(s["x1"], s["x2"], go, 9, 1, 9, 1, 2),
+                               sets, args.iters)
+            print(json.dumps(dict(level=l, op="corr_bwd", shape=[B, C, h, w],
+                                  med_us=round(med, 2), mean_us=round(mean, 2))))
+            gw = torch.randn(B, C, h, w, device=dev)
+            med, mean = timeit(lambda s: warp_backward(s["x2"], s["fl"], gw), sets, args.iters)
+            print(json.dumps(dict(level=l, op="warp_bwd", shape=[B, C, h, w],
+                                  med_us=round(med, 2), mean_us=round(mean, 2))))
+
+
+if __name__ == "__main__":
+    main()
