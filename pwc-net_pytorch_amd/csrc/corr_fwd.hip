@@ -259,212 +259,6 @@ __global__ __launch_bounds__(G::THREADS) void corr_fwd_tiled(
   }
 }
 
-// ------------------------------------------------------------------------------------
-// LDS-DMA ring kernel (k == 1, s1 == 1, TX + 2*DR*S == 32, W % 4 == 0, aligned tiles).
-//
-// The f1 tile (TY x 16) and the f2 tile ((TY+2*HALO) x 32) of CC channels form one stage;
-// stages are filled by global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR
-// staging) into an NS-deep LDS ring, so NS-1 stages (NS-1 x CC x 5 KiB) are in flight per
-// workgroup while the previous stage is consumed.  Out-of-image quads are sourced from a
-// 16-byte zero page (the reference's zero padding, correlation_cuda.c:40-41).  f2 rows are
-// stored unpadded with the quad index XOR-swizzled by bit 1 of the row (swizzle applied on the
-// DMA source address, linear LDS destination), which makes the 4-row ds_read_b128 lane groups
-// conflict-free.  Waves wait on their own DMA with a counted vmcnt and meet at a raw
-// s_barrier (a __syncthreads() would drain every in-flight DMA).
-// ------------------------------------------------------------------------------------
-__device__ __attribute__((aligned(16))) float g_zero_quad[4];
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t lds_addr(const float* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
-}
-
-// Six ds_read_b128 and their lgkmcnt(0) in ONE asm statement.  Compiler-visible LDS loads
-// would each be preceded by an s_waitcnt vmcnt(0) (hipcc cannot prove they do not alias the
-// in-flight LDS-DMA of later stages), which drains the ring every channel; the asm loads are
-// ordered after the stage's barrier by the "memory" clobber, and their results are complete
-// when the statement ends.
-__device__ __forceinline__ void lds_read6(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                          uint32_t a4, uint32_t a5, f32x4& r0, f32x4& r1,
-                                          f32x4& r2, f32x4& r3, f32x4& r4, f32x4& r5) {
-  asm volatile(
-      "ds_read_b128 %0, %6\n\t"
-      "ds_read_b128 %1, %7\n\t"
-      "ds_read_b128 %2, %8\n\t"
-      "ds_read_b128 %3, %9\n\t"
-      "ds_read_b128 %4, %10\n\t"
-      "ds_read_b128 %5, %11\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5)
-      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5)
-      : "memory");
-}
-
-template <int DR_, int S_, int TY_, int CC_, int NS_, int PPW_>
-struct RingTile {
-  static constexpr int DR = DR_, S = S_, TY = TY_, CC = CC_, NS = NS_, PPW = PPW_;
-  static constexpr int D = 2 * DR + 1;
-  static constexpr int HALO = DR * S;
-  static constexpr int TX = 16, NQ = 4, PX = 4;
-  static constexpr int X2 = 32;  // f2 tile row: 8 quads
-  static constexpr int R2 = TY + 2 * HALO;
-  static constexpr int NWQ = (PX + 2 * DR * S) / 4;  // f2 window quads per lane
-  static constexpr int THREADS = TY * NQ * D;
-  static constexpr int F2_FLOATS = R2 * X2;
-  static constexpr int F1_FLOATS = TY * TX;
-  static constexpr int CH_FLOATS = F2_FLOATS + F1_FLOATS;
-  static constexpr int STAGE_FLOATS = CC * CH_FLOATS;
-  static constexpr int LDS_BYTES = NS * STAGE_FLOATS * 4;
-  static constexpr int F2P = R2 / 8;   // 1 KiB pieces per channel (8 rows of 8 quads)
-  static constexpr int F1P = TY / 16;  // 16 rows of 4 quads
-  static constexpr int PIECES = CC * (F2P + F1P);
-  static constexpr int ISSUERS = PIECES / PPW;
-  static_assert(TX + 2 * HALO == X2, "ring tile needs a 32-float f2 row");
-  static_assert(R2 % 8 == 0 && TY % 16 == 0, "whole 1 KiB pieces");
-  static_assert(PIECES % PPW == 0, "uniform pieces per issuing wave");
-  static_assert(ISSUERS <= THREADS / 64, "enough waves to issue");
-  static_assert((NWQ - 1) + (NQ - 1) < 8, "window inside the row");
-  static_assert(THREADS % 64 == 0 && THREADS <= 1024, "workgroup");
-  static_assert(NS >= 2, "ring depth");
-};
-
-template <class G, typename T>
-__device__ __forceinline__ void ring_issue(float* lds, int stage, int c0, const T* __restrict__ f1n,
-                                           const T* __restrict__ f2n, int C, int H, int W,
-                                           int y1, int x1, int wave, int lane) {
-  static_assert(sizeof(T) == 4, "ring kernel streams fp32");
-  if (wave >= G::ISSUERS) return;
-  float* sbase = lds + (stage % G::NS) * G::STAGE_FLOATS;
-  const size_t plane = (size_t)H * W;
-#pragma unroll
-  for (int i = 0; i < G::PPW; ++i) {
-    const int p = wave * G::PPW + i;
-    const int cc = p / (G::F2P + G::F1P);
-    const int k = p % (G::F2P + G::F1P);
-    const int c = c0 + cc;
-    float* dst = sbase + cc * G::CH_FLOATS;
-    int gy, gx;
-    if (k < G::F2P) {
-      const int r = 8 * k + (lane >> 3);
-      const int srcq = (lane & 7) ^ (((r >> 1) & 1) << 2);
-      gy = y1 - G::HALO + r;
-      gx = x1 - G::HALO + 4 * srcq;
-      dst += 8 * k * G::X2;
-    } else {
-      gy = y1 + (lane >> 2);
-      gx = x1 + 4 * (lane & 3);
-      dst += G::F2_FLOATS;
-    }
-    const T* base = (k < G::F2P) ? f2n : f1n;
-    const bool ok = c < C && gy >= 0 && gy < H && gx >= 0 && gx < W;
-    const float* src = ok ? reinterpret_cast<const float*>(base + (size_t)c * plane +
-                                                           (size_t)gy * W + gx)
-                          : g_zero_quad;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-  }
-}
-
-template <class G, typename T>
-__global__ __launch_bounds__(G::THREADS, 5) void corr_fwd_ring(
-    const T* __restrict__ in1, const T* __restrict__ in2, T* __restrict__ out, int B, int C,
-    int H, int W, int Ho, int Wo, int off, int layout, float divisor, int n_ty, int n_tx) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int tx_tile = t % n_tx;
-  const int ty_tile = (t / n_tx) % n_ty;
-  const int n = t / (n_tx * n_ty);
-  const int oy0 = ty_tile * G::TY, ox0 = tx_tile * G::TX;
-  const int y1 = oy0 + off, x1 = ox0 + off;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int q = threadIdx.x % G::NQ;
-  const int ty = (threadIdx.x / G::NQ) % G::TY;
-  const int tjx = threadIdx.x / (G::NQ * G::TY);  // == wave for TY*NQ == 64
-
-  const size_t plane = (size_t)H * W;
-  const T* f1n = in1 + (size_t)n * C * plane;
-  const T* f2n = in2 + (size_t)n * C * plane;
-
-  // lane-constant LDS float offsets within a channel block
-  const int r2 = ty + G::S * tjx;
-  const int sw = ((r2 >> 1) & 1) << 2;
-  int woff[G::NWQ];
-#pragma unroll
-  for (int u = 0; u < G::NWQ; ++u) woff[u] = r2 * G::X2 + (((q + u) ^ sw) << 2);
-  const int aoff = G::F2_FLOATS + ty * G::TX + (q << 2);
-  const uint32_t lds_base = lds_addr(lds);
-
-  float acc[G::D][G::PX];
-#pragma unroll
-  for (int a = 0; a < G::D; ++a)
-#pragma unroll
-    for (int k = 0; k < G::PX; ++k) acc[a][k] = 0.f;
-
-  const int nst = (C + G::CC - 1) / G::CC;
-#pragma unroll
-  for (int s = 0; s < G::NS - 1; ++s)
-    if (s < nst) ring_issue<G, T>(lds, s, s * G::CC, f1n, f2n, C, H, W, y1, x1, wave, lane);
-
-  for (int st = 0; st < nst; ++st) {
-    if (wave < G::ISSUERS) {
-      if (nst - 1 - st >= G::NS - 2)
-        wait_vmcnt<(G::NS - 2) * G::PPW>();
-      else
-        wait_vmcnt<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (st + G::NS - 1 < nst)
-      ring_issue<G, T>(lds, st + G::NS - 1, (st + G::NS - 1) * G::CC, f1n, f2n, C, H, W, y1,
-                       x1, wave, lane);
-    const uint32_t sb = lds_base + (uint32_t)((st % G::NS) * G::STAGE_FLOATS * 4);
-#pragma unroll 1  // one channel live: 2 workgroups/CU
-    for (int cc = 0; cc < G::CC; ++cc) {
-      const uint32_t cb = sb + (uint32_t)(cc * G::CH_FLOATS * 4);
-      f32x4 a4, b[G::NWQ];
-      static_assert(G::NWQ == 5, "lds_read6 reads the f1 quad + 5 window quads");
-      lds_read6(cb + aoff * 4, cb + woff[0] * 4, cb + woff[1] * 4, cb + woff[2] * 4,
-                cb + woff[3] * 4, cb + woff[4] * 4, a4, b[0], b[1], b[2], b[3], b[4]);
-      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-      float w[4 * G::NWQ];
-#pragma unroll
-      for (int u = 0; u < G::NWQ; ++u) {
-        w[4 * u + 0] = b[u].x;
-        w[4 * u + 1] = b[u].y;
-        w[4 * u + 2] = b[u].z;
-        w[4 * u + 3] = b[u].w;
-      }
-#pragma unroll
-      for (int ti = 0; ti < G::D; ++ti)
-#pragma unroll
-        for (int k = 0; k < G::PX; ++k) acc[ti][k] = fmaf(av[k], w[k + G::S * ti], acc[ti][k]);
-    }
-  }
-
-  const int oy = oy0 + ty;
-  const int ox = ox0 + 4 * q;
-  if (oy >= Ho || ox >= Wo) return;
-  const int OC = G::D * G::D;
-  const int tj = tjx - G::DR;
-#pragma unroll
-  for (int ti = 0; ti < G::D; ++ti) {
-    const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
-    T* orow = out + (((size_t)n * OC + oc) * Ho + oy) * Wo;
-    const float4 v = make_float4(acc[ti][0] / divisor, acc[ti][1] / divisor,
-                                 acc[ti][2] / divisor, acc[ti][3] / divisor);
-    *reinterpret_cast<float4*>(orow + ox) = v;
-  }
-}
-
 // Generic kernel: one thread per output element, literal cu:34-106 arithmetic.
 template <typename T>
 __global__ void corr_fwd_generic(const T* __restrict__ in1, const T* __restrict__ in2,
@@ -549,36 +343,10 @@ static hipError_t launch_generic(const void* in1, const void* in2, void* out, in
   return hipGetLastError();
 }
 
-using Ring9 = RingTile</*DR*/ 4, /*S*/ 2, /*TY*/ 16, /*CC*/ 4, /*NS*/ 4, /*PPW*/ 4>;
-
-template <class G>
-static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B, int C, int H,
-                              int W, int Ho, int Wo, int off, int layout, float divisor,
-                              hipStream_t stream) {
-  const int n_ty = (Ho + G::TY - 1) / G::TY;
-  const int n_tx = (Wo + G::TX - 1) / G::TX;
-  const long long nblk = (long long)B * n_ty * n_tx;
-  if (nblk <= 0) return hipSuccess;
-  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&corr_fwd_ring<G, float>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((corr_fwd_ring<G, float>), dim3((unsigned)nblk), dim3(G::THREADS),
-                     G::LDS_BYTES, stream, (const float*)in1, (const float*)in2, (float*)out, B,
-                     C, H, W, Ho, Wo, off, layout, divisor, n_ty, n_tx);
-  return hipGetLastError();
-}
-
-// The ring kernel needs whole, 16-byte aligned quads everywhere it touches memory.
-static bool ring_ok(const void* in1, const void* in2, const void* out, int W, int Wo, int off) {
-  return W % 4 == 0 && Wo % 4 == 0 && off % 4 == 0 && (uintptr_t)in1 % 16 == 0 &&
-         (uintptr_t)in2 % 16 == 0 && (uintptr_t)out % 16 == 0;
-}
+// corr_ring.hip
+hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, int B, int C,
+                                 int H, int W, int Ho, int Wo, int off, int dr, int s2,
+                                 int layout, float divisor, hipStream_t stream);
 
 template <typename T>
 hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, int C, int H,
@@ -586,13 +354,10 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
                           int layout, float divisor, hipStream_t stream, int force_generic) {
   const int kr = (k - 1) / 2;
   const int dr = md / s2;
-  if (force_generic != 1 && k == 1 && s1 == 1 && sizeof(T) == 4 && force_generic != 2) {
-    const int off = md - pad;
-    if (ring_ok(in1, in2, out, W, Wo, off)) {
-      if (dr == 4 && s2 == 2)
-        return launch_ring<Ring9>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor,
-                                  stream);
-    }
+  if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4) {
+    const hipError_t e = corr_forward_ring_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad, dr,
+                                               s2, layout, divisor, stream);
+    if (e != hipErrorNotSupported) return e;
   }
   if (force_generic != 1 && k == 1 && s1 == 1 && dr == 4) {
     const int off = md - pad;

@@ -1,0 +1,309 @@
+// corr_ring.hip — correlation forward, LDS-DMA ring kernel for gfx950 (the l4 / "level 2" path).
+//
+// Semantics: correlation_cuda_kernel.cu:34-106 of daigo0927/PWC-Net_pytorch with
+// kernel_size 1, stride1 1 (model.py:24 builds Correlation(9, 1, 9, 1, 2)):
+//   out[n, tc, oy, ox] = sum_c f1[n,c,oy+off,ox+off] * f2[n,c,oy+off+tj*S,ox+off+ti*S] / divisor
+// with zeros outside the image (the reference's zero-filled padded scratch), off = md - pad.
+//
+// Structure (one workgroup = one 16x16 output tile of one image, 9 waves = one displacement row
+// tj each; lane = (output row ty, 4-pixel group q)):
+//   * the f1 tile (16x16) and the f2 tile (16+2*HALO rows x 32 columns) of CC channels form a
+//     stage; stages are streamed HBM/L2 -> LDS by buffer_load_dwordx4 ... lds (LDS-DMA, 1 KiB
+//     per wave-instruction, no VGPR staging) into an NS-deep ring, so NS-1 stages are in flight
+//     while one is consumed;
+//   * out-of-image quads get a voffset past the buffer's num_records, which the buffer unit
+//     turns into zeros (the reference's zero padding) -- no branches, no zero page;
+//   * f2 rows are stored unpadded with the quad index XOR-swizzled by bit 1 of the row
+//     (swizzle applied to the DMA source, LDS destination linear), so the four rows a
+//     ds_read_b128 lane group touches hit disjoint 16-bank slices (measured 0 conflicts);
+//   * each lane reads its f1 quad + 5 f2 quads per channel (6 x ds_read_b128, in one asm
+//     statement: compiler-visible LDS loads would each get an s_waitcnt vmcnt(0) because hipcc
+//     cannot prove they miss the in-flight DMA) and runs 36 FMAs (4 pixels x 9 ti);
+//   * waves wait on their own DMA with a counted vmcnt and meet at a raw s_barrier (a
+//     __syncthreads() would drain every in-flight stage);
+//   * tiles are remapped XCD-aware so neighbouring tiles (shared halo rows) share an L2.
+#include <cstdlib>
+#include <cstring>
+
+#include "pwc_common.cuh"
+
+namespace pwc {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// Six ds_read_b128 + lgkmcnt(0) in one statement (see file header).
+__device__ __forceinline__ void lds_read6(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                          uint32_t a4, uint32_t a5, f32x4& r0, f32x4& r1,
+                                          f32x4& r2, f32x4& r3, f32x4& r4, f32x4& r5) {
+  asm volatile(
+      "ds_read_b128 %0, %6\n\t"
+      "ds_read_b128 %1, %7\n\t"
+      "ds_read_b128 %2, %8\n\t"
+      "ds_read_b128 %3, %9\n\t"
+      "ds_read_b128 %4, %10\n\t"
+      "ds_read_b128 %5, %11\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5)
+      : "memory");
+}
+
+template <int DR_, int S_, int TY_, int CC_, int NS_, int PPW_>
+struct RingTile {
+  static constexpr int DR = DR_, S = S_, TY = TY_, CC = CC_, NS = NS_, PPW = PPW_;
+  static constexpr int D = 2 * DR + 1;
+  static constexpr int HALO = DR * S;
+  static constexpr int TX = 16, NQ = 4, PX = 4;
+  static constexpr int X2 = 32;  // f2 tile row: 8 quads
+  static constexpr int R2 = TY + 2 * HALO;
+  static constexpr int NWQ = (PX + 2 * DR * S) / 4;  // f2 window quads per lane
+  static constexpr int THREADS = TY * NQ * D;
+  static constexpr int F2_FLOATS = R2 * X2;
+  static constexpr int F1_FLOATS = TY * TX;
+  static constexpr int CH_FLOATS = F2_FLOATS + F1_FLOATS;
+  static constexpr int STAGE_FLOATS = CC * CH_FLOATS;
+  static constexpr int LDS_BYTES = NS * STAGE_FLOATS * 4;
+  static constexpr int F2P = R2 / 8;   // 1 KiB pieces per channel (8 rows of 8 quads)
+  static constexpr int F1P = TY / 16;  // 16 rows of 4 quads
+  static constexpr int PIECES = CC * (F2P + F1P);
+  static constexpr int ISSUERS = PIECES / PPW;
+  static_assert(TX + 2 * HALO == X2, "ring tile needs a 32-float f2 row");
+  static_assert(R2 % 8 == 0 && TY % 16 == 0, "whole 1 KiB pieces");
+  static_assert(PIECES % PPW == 0, "uniform pieces per issuing wave");
+  static_assert(ISSUERS <= THREADS / 64, "enough waves to issue");
+  static_assert(NWQ == 5, "lds_read6: one f1 quad + five f2 quads");
+  static_assert((NWQ - 1) + (NQ - 1) < 8, "window inside the row");
+  static_assert(THREADS % 64 == 0 && THREADS <= 1024, "workgroup");
+  static_assert(NS >= 2, "ring depth");
+};
+
+template <class G>
+__device__ __forceinline__ void ring_issue(int stage, int wave, uint32_t plane, uint32_t lds0,
+                                           __amdgpu_buffer_rsrc_t rs1,
+                                           __amdgpu_buffer_rsrc_t rs2,
+                                           const uint32_t (&src_off)[G::PPW],
+                                           const uint32_t (&dst_off)[G::PPW],
+                                           const bool (&from_f2)[G::PPW]) {
+  constexpr uint32_t kOOB = 0x80000000u;
+  if (wave >= G::ISSUERS) return;
+  const uint32_t cbytes = (uint32_t)(stage * G::CC) * plane * 4u;  // channel advance
+  const uint32_t sbase = lds0 + (uint32_t)((stage % G::NS) * G::STAGE_FLOATS) * 4u;
+#pragma unroll
+  for (int i = 0; i < G::PPW; ++i) {
+    // channels past C land at offsets >= num_records: zeros from the range check
+    const uint32_t vo = src_off[i] == kOOB ? kOOB : src_off[i] + cbytes;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        from_f2[i] ? rs2 : rs1,
+        (__attribute__((address_space(3))) void*)(uintptr_t)(sbase + dst_off[i]), 16, vo, 0, 0,
+        0);
+  }
+}
+
+template <class G>
+__global__ __launch_bounds__(G::THREADS, 5) void corr_fwd_ring(
+    const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
+    int C, int H, int W, int Ho, int Wo, int off, int layout, float divisor, float inv_divisor,
+    int n_ty, int n_tx) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tx_tile = t % n_tx;
+  const int ty_tile = (t / n_tx) % n_ty;
+  const int n = t / (n_tx * n_ty);
+  const int oy0 = ty_tile * G::TY, ox0 = tx_tile * G::TX;
+  const int y1 = oy0 + off, x1 = ox0 + off;  // f1 tile origin, unpadded image coordinates
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = threadIdx.x % G::NQ;
+  const int ty = (threadIdx.x / G::NQ) % G::TY;
+  const int tjx = threadIdx.x / (G::NQ * G::TY);
+
+  const uint32_t plane = (uint32_t)(H * W);
+  const uint32_t img_bytes = (uint32_t)C * plane * 4u;  // checked < 2^31 by the launcher
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(in1 + (size_t)n * C * plane), (short)0, (int)img_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(in2 + (size_t)n * C * plane), (short)0, (int)img_bytes, 0x00020000);
+  const uint32_t lds0 = lds_addr(lds);
+
+  // ---- DMA issue plan: issuer wave w owns pieces w*PPW .. w*PPW+PPW-1 of every stage ----
+  // per piece: source byte offset of this lane for channel 0 (or OOB), LDS byte offset.
+  uint32_t src_off[G::PPW];
+  uint32_t dst_off[G::PPW];
+  bool from_f2[G::PPW];
+  constexpr uint32_t kOOB = 0x80000000u;  // >= num_records: the buffer unit returns zeros
+  if (wave < G::ISSUERS) {
+#pragma unroll
+    for (int i = 0; i < G::PPW; ++i) {
+      const int p = wave * G::PPW + i;
+      const int cc = p / (G::F2P + G::F1P);
+      const int k = p % (G::F2P + G::F1P);
+      int gy, gx;
+      uint32_t dst = (uint32_t)(cc * G::CH_FLOATS) * 4u;
+      if (k < G::F2P) {
+        const int r = 8 * k + (lane >> 3);
+        const int srcq = (lane & 7) ^ (((r >> 1) & 1) << 2);
+        gy = y1 - G::HALO + r;
+        gx = x1 - G::HALO + 4 * srcq;
+        dst += (uint32_t)(8 * k * G::X2) * 4u;
+      } else {
+        gy = y1 + (lane >> 2);
+        gx = x1 + 4 * (lane & 3);
+        dst += (uint32_t)G::F2_FLOATS * 4u;
+      }
+      const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+      src_off[i] = ok ? ((uint32_t)cc * plane + (uint32_t)(gy * W + gx)) * 4u : kOOB;
+      dst_off[i] = dst;
+      from_f2[i] = k < G::F2P;
+    }
+  }
+  // ---- lane-constant LDS read offsets (bytes, relative to a channel block) ----
+  const int r2 = ty + G::S * tjx;
+  const int sw = ((r2 >> 1) & 1) << 2;
+  uint32_t woff[G::NWQ];
+#pragma unroll
+  for (int u = 0; u < G::NWQ; ++u) woff[u] = (uint32_t)(r2 * G::X2 + (((q + u) ^ sw) << 2)) * 4u;
+  const uint32_t aoff = (uint32_t)(G::F2_FLOATS + ty * G::TX + (q << 2)) * 4u;
+
+  float acc[G::D][G::PX];
+#pragma unroll
+  for (int a = 0; a < G::D; ++a)
+#pragma unroll
+    for (int k = 0; k < G::PX; ++k) acc[a][k] = 0.f;
+
+  const int nst = (C + G::CC - 1) / G::CC;
+#pragma unroll
+  for (int s = 0; s < G::NS - 1; ++s)
+    if (s < nst) ring_issue<G>(s, wave, plane, lds0, rs1, rs2, src_off, dst_off, from_f2);
+
+  for (int st = 0; st < nst; ++st) {
+    if (wave < G::ISSUERS) {
+      if (nst - 1 - st >= G::NS - 2)
+        wait_vmcnt<(G::NS - 2) * G::PPW>();
+      else
+        wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (st + G::NS - 1 < nst)
+      ring_issue<G>(st + G::NS - 1, wave, plane, lds0, rs1, rs2, src_off, dst_off, from_f2);
+    const uint32_t sb = lds0 + (uint32_t)((st % G::NS) * G::STAGE_FLOATS) * 4u;
+#pragma unroll 1  // one channel's operands live at a time: 96 VGPRs, 2 workgroups/CU
+    for (int cc = 0; cc < G::CC; ++cc) {
+      const uint32_t cb = sb + (uint32_t)(cc * G::CH_FLOATS) * 4u;
+      f32x4 a4, b[G::NWQ];
+      lds_read6(cb + aoff, cb + woff[0], cb + woff[1], cb + woff[2], cb + woff[3], cb + woff[4],
+                a4, b[0], b[1], b[2], b[3], b[4]);
+      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+      float w[4 * G::NWQ];
+#pragma unroll
+      for (int u = 0; u < G::NWQ; ++u) {
+        w[4 * u + 0] = b[u].x;
+        w[4 * u + 1] = b[u].y;
+        w[4 * u + 2] = b[u].z;
+        w[4 * u + 3] = b[u].w;
+      }
+#pragma unroll
+      for (int ti = 0; ti < G::D; ++ti)
+#pragma unroll
+        for (int k = 0; k < G::PX; ++k) acc[ti][k] = fmaf(av[k], w[k + G::S * ti], acc[ti][k]);
+    }
+  }
+
+  // ---- epilogue: out = acc / divisor (cu:100); a power-of-two divisor is an exact scale ----
+  const int oy = oy0 + ty;
+  const int ox = ox0 + 4 * q;
+  if (oy >= Ho || ox >= Wo) return;
+  const int OC = G::D * G::D;
+  const int tj = tjx - G::DR;
+  const bool pow2 = inv_divisor != 0.f;
+#pragma unroll
+  for (int ti = 0; ti < G::D; ++ti) {
+    const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
+    float* orow = out + (((size_t)n * OC + oc) * Ho + oy) * Wo;
+    float4 v;
+    if (pow2)
+      v = make_float4(acc[ti][0] * inv_divisor, acc[ti][1] * inv_divisor,
+                      acc[ti][2] * inv_divisor, acc[ti][3] * inv_divisor);
+    else
+      v = make_float4(acc[ti][0] / divisor, acc[ti][1] / divisor, acc[ti][2] / divisor,
+                      acc[ti][3] / divisor);
+    *reinterpret_cast<float4*>(orow + ox) = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// configurations (CC channels per stage, NS ring depth); selectable for measurement with
+// PWC_RING_CFG=<name> (read once).  LDS = NS * CC * 5 KiB.
+// ------------------------------------------------------------------------------------
+using RingA = RingTile<4, 2, 16, 4, 3, 4>;  // 60 KiB, 2 stages in flight
+using RingB = RingTile<4, 2, 16, 4, 4, 4>;  // 80 KiB, 3 in flight
+using RingC = RingTile<4, 2, 16, 2, 6, 2>;  // 60 KiB, 5 in flight
+using RingD = RingTile<4, 2, 16, 3, 5, 3>;  // 75 KiB, 4 in flight
+using RingE = RingTile<4, 2, 16, 2, 8, 2>;  // 80 KiB, 7 in flight
+
+template <class G>
+static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B, int C, int H,
+                              int W, int Ho, int Wo, int off, int layout, float divisor,
+                              hipStream_t stream) {
+  const int n_ty = (Ho + G::TY - 1) / G::TY;
+  const int n_tx = (Wo + G::TX - 1) / G::TX;
+  const long long nblk = (long long)B * n_ty * n_tx;
+  if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_ring<G>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  // exact reciprocal when the divisor is a power of two (then x * inv == x / divisor)
+  int ex;
+  const float m = std::frexp(divisor, &ex);
+  const float inv = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
+  hipLaunchKernelGGL((corr_fwd_ring<G>), dim3((unsigned)nblk), dim3(G::THREADS), G::LDS_BYTES,
+                     stream, (const float*)in1, (const float*)in2, (float*)out, C, H, W, Ho,
+                     Wo, off, layout, divisor, inv, n_ty, n_tx);
+  return hipGetLastError();
+}
+
+static int ring_cfg() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = std::getenv("PWC_RING_CFG");
+    v = 1;  // default: B
+    if (s && s[0] >= 'A' && s[0] <= 'E' && s[1] == 0) v = s[0] - 'A';
+  }
+  return v;
+}
+
+// hipErrorNotSupported: shape / alignment outside what the ring kernel handles.
+hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, int B, int C,
+                                 int H, int W, int Ho, int Wo, int off, int dr, int s2,
+                                 int layout, float divisor, hipStream_t stream) {
+  if (!(dr == 4 && s2 == 2)) return hipErrorNotSupported;
+  if (W % 4 || Wo % 4 || off % 4) return hipErrorNotSupported;
+  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16)
+    return hipErrorNotSupported;
+  if ((size_t)C * H * W * 4 >= 0x7ffffff0ull) return hipErrorNotSupported;
+  switch (ring_cfg()) {
+    case 0: return launch_ring<RingA>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    case 2: return launch_ring<RingC>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    case 3: return launch_ring<RingD>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    case 4: return launch_ring<RingE>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    default: return launch_ring<RingB>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+  }
+}
+
+}  // namespace pwc

@@ -16,22 +16,22 @@ namespace pwc {
 
 // torch.linspace(-1, 1, n)[i] in fp32 (ATen RangeFactories: step = (end-start)/(n-1),
 // lower half start + step*i, upper half end - step*(n-1-i)).
-// hipcc lowers __fmul_rn/__fadd_rn to plain operators, so contraction is disabled explicitly
-// in the coordinate chain: an fma there would round differently from the reference.
+// Contraction is disabled in this scope with plain operators: hipcc's __fmul_rn/__fadd_rn are
+// plain operators defined in a header (outside this pragma), so they would still be fused,
+// and an fma here rounds differently from the reference's separate fp32 ops.
 __device__ __forceinline__ float linspace_m1p1(int i, int n) {
 #pragma clang fp contract(off)
   if (n == 1) return -1.f;
-  const float step = __fdiv_rn(2.f, (float)(n - 1));
-  return (i < n / 2) ? __fadd_rn(-1.f, __fmul_rn(step, (float)i))
-                     : __fsub_rn(1.f, __fmul_rn(step, (float)(n - 1 - i)));
+  const float step = 2.f / (float)(n - 1);
+  return (i < n / 2) ? -1.f + step * (float)i : 1.f - step * (float)(n - 1 - i);
 }
 
 // Source coordinate of the reference chain for one axis.  `half` = (size-1.0)/2.0 computed in
 // double on the host (Python float), divided in fp32 like tensor / python-float.
 __device__ __forceinline__ float src_coord(float disp, int i, int n, float half) {
 #pragma clang fp contract(off)
-  const float g = __fadd_rn(linspace_m1p1(i, n), __fdiv_rn(disp, half));
-  return __fmul_rn(__fdiv_rn(__fadd_rn(g, 1.f), 2.f), (float)(n - 1));
+  const float g = linspace_m1p1(i, n) + disp / half;
+  return ((g + 1.f) / 2.f) * (float)(n - 1);
 }
 
 struct Bilinear {
@@ -47,10 +47,10 @@ __device__ __forceinline__ Bilinear bilinear(float ix, float iy, int H, int W) {
   b.x0 = (int)fx;
   b.y0 = (int)fy;
   // ATen: nw = (ix_se - ix) * (iy_se - iy) etc.
-  b.wx1 = __fsub_rn(ix, fx);
-  b.wx0 = __fsub_rn(fx + 1.f, ix);
-  b.wy1 = __fsub_rn(iy, fy);
-  b.wy0 = __fsub_rn(fy + 1.f, iy);
+  b.wx1 = ix - fx;
+  b.wx0 = (fx + 1.f) - ix;
+  b.wy1 = iy - fy;
+  b.wy0 = (fy + 1.f) - iy;
   b.vx0 = b.x0 >= 0 && b.x0 < W;
   b.vx1 = b.x0 + 1 >= 0 && b.x0 + 1 < W;
   b.vy0 = b.y0 >= 0 && b.y0 < H;
@@ -103,8 +103,8 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
   const float iy = src_coord(v, py, H, halfy);
   const Bilinear b = bilinear(ix, iy, H, W);
   const Corners k = corners(b, H, W);
-  const float w00 = __fmul_rn(b.wx0, b.wy0), w01 = __fmul_rn(b.wx1, b.wy0);
-  const float w10 = __fmul_rn(b.wx0, b.wy1), w11 = __fmul_rn(b.wx1, b.wy1);
+  const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;  // feed fma operands: not fusable
+  const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
   const int c0 = blockIdx.y * CB;
   float r[CB][4];
 #pragma unroll

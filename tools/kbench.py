@@ -22,19 +22,25 @@ from pwcnet_amd.ops import corr_backward, corr_forward, warp_backward, warp_forw
 
 
 def timeit(fn, sets, iters):
+    """Mean device time per launch over `iters` back-to-back launches (rotating buffer sets)
+    between two events, repeated 5 times; returns (median-of-5, min-of-5) in microseconds.
+    Back-to-back launches keep the queue full, so host launch latency is not measured (the
+    ~1-2 us inter-kernel gap of the GPU is)."""
     for s in sets:
         fn(s)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(iters)]
-    for i, (a, b) in enumerate(evs):
-        s = sets[i % len(sets)]
+    res = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(2_000_000)  # let the host enqueue ahead of the device
         a.record()
-        fn(s)
+        for i in range(iters):
+            fn(sets[i % len(sets)])
         b.record()
-    torch.cuda.synchronize()
-    ts = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
-    return ts[len(ts) // 2], sum(ts) / len(ts)
+        torch.cuda.synchronize()
+        res.append(a.elapsed_time(b) * 1e3 / iters)
+    res.sort()
+    return res[2], res[0]
 
 
 def main():
@@ -45,13 +51,17 @@ def main():
     ap.add_argument("--iters", type=int, default=60)
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--backward", action="store_true")
+    ap.add_argument("--levels", default="0,1,2,3,4")
     args = ap.parse_args()
     dt = torch.float32 if args.dtype == "fp32" else torch.float16
     esz = 4 if dt == torch.float32 else 2
     dev = torch.device("cuda:0")
     B = args.batch
     path = os.environ.get("PWC_CORR_PATH", "default")
+    levels = [int(v) for v in args.levels.split(",")]
     for l, (C, h, w) in enumerate(bench.level_shapes(args.height, args.width)):
+        if l not in levels:
+            continue
         per = (3 * C * h * w + 83 * h * w) * B * esz
         n = max(2, int(2 * 256 * 2 ** 20 / per) + 1)
         g = torch.Generator(device=dev).manual_seed(l)
@@ -63,22 +73,22 @@ def main():
                            args.iters)
         cb = bench.corr_bytes_per_pair(C, h, w, esz) * B
         print(json.dumps(dict(level=l, op="corr_fwd", path=path, shape=[B, C, h, w],
-                              med_us=round(med, 2), mean_us=round(mean, 2),
+                              us=round(med, 2), min_us=round(mean, 2),
                               gbs=round(cb / (med * 1e-6) / 1e9, 1))))
         med, mean = timeit(lambda s: warp_forward(s["x2"], s["fl"]), sets, args.iters)
         wb = (2 * C * h * w + 2 * h * w) * B * esz
-        print(json.dumps(dict(level=l, op="warp_fwd", shape=[B, C, h, w], med_us=round(med, 2),
-                              mean_us=round(mean, 2), gbs=round(wb / (med * 1e-6) / 1e9, 1))))
+        print(json.dumps(dict(level=l, op="warp_fwd", shape=[B, C, h, w], us=round(med, 2),
+                              min_us=round(mean, 2), gbs=round(wb / (med * 1e-6) / 1e9, 1))))
         if args.backward and dt == torch.float32:
             go = torch.randn(B, 81, h, w, device=dev)
             med, mean = timeit(lambda s: corr_backward(s["x1"], s["x2"], go, 9, 1, 9, 1, 2),
                                sets, args.iters)
             print(json.dumps(dict(level=l, op="corr_bwd", shape=[B, C, h, w],
-                                  med_us=round(med, 2), mean_us=round(mean, 2))))
+                                  us=round(med, 2), min_us=round(mean, 2))))
             gw = torch.randn(B, C, h, w, device=dev)
             med, mean = timeit(lambda s: warp_backward(s["x2"], s["fl"], gw), sets, args.iters)
             print(json.dumps(dict(level=l, op="warp_bwd", shape=[B, C, h, w],
-                                  med_us=round(med, 2), mean_us=round(mean, 2))))
+                                  us=round(med, 2), min_us=round(mean, 2))))
 
 
 if __name__ == "__main__":
