@@ -37,6 +37,8 @@
 #define PWC_API
 #endif
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -46,7 +48,7 @@ extern "C" {
 #define PWC_DTYPE_F16 1
 #define PWC_DTYPE_BF16 2
 
-/* ABI version; bumped on any signature change. */
+/* ABI version; bumped on any signature change (2: workspace entry points). */
 PWC_API int pwc_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -65,6 +67,17 @@ PWC_API int pwc_corr_forward(const void* in1, const void* in2, void* out, int B,
                      int pad_size, int kernel_size, int max_displacement, int stride1,
                      int stride2, int corr_multiply, int dtype, void* stream);
 
+/* Same as pwc_corr_forward with a caller-owned device workspace of at least
+ * pwc_corr_workspace_size() bytes.  For grids too small to fill the GPU (coarse pyramid
+ * levels) the channel sum is split across workgroups into partial volumes in `workspace` and
+ * reduced in a fixed order (deterministic).  A size of 0 means no workspace is used. */
+PWC_API size_t pwc_corr_workspace_size(int B, int C, int H, int W, int pad_size, int kernel_size,
+                               int max_displacement, int stride1, int stride2);
+PWC_API int pwc_corr_forward_ws(const void* in1, const void* in2, void* out, int B, int C, int H,
+                        int W, int pad_size, int kernel_size, int max_displacement,
+                        int stride1, int stride2, int corr_multiply, int dtype,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
 /* grad_in1/grad_in2 ([B][C][H][W]) from grad_out ([B][OC][Ho][Wo]) exactly as
  * correlation_cuda_kernel.cu:108-290.  Requires stride1 == 1 (the reference backward is
  * undefined otherwise: it indexes gradInput with the strided coordinate).  Every element of
@@ -78,6 +91,10 @@ PWC_API int pwc_corr_backward(const void* in1, const void* in2, const void* grad
  * modules.py:58-72, value sum_c src*tgt(shifted) / (2sr+1)^2. */
 PWC_API int pwc_cost_volume_forward(const void* src, const void* tgt, void* out, int B, int C, int H,
                             int W, int search_range, int dtype, void* stream);
+PWC_API size_t pwc_cost_volume_workspace_size(int B, int C, int H, int W, int search_range);
+PWC_API int pwc_cost_volume_forward_ws(const void* src, const void* tgt, void* out, int B, int C,
+                               int H, int W, int search_range, int dtype, void* workspace,
+                               size_t workspace_bytes, void* stream);
 PWC_API int pwc_cost_volume_backward(const void* src, const void* tgt, const void* grad_out,
                              void* grad_src, void* grad_tgt, int B, int C, int H, int W,
                              int search_range, int dtype, void* stream);

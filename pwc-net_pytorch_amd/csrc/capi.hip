@@ -13,7 +13,8 @@
 namespace pwc {
 template <typename T>
 hipError_t corr_forward_t(const void*, const void*, void*, int, int, int, int, int, int, int,
-                          int, int, int, int, int, float, hipStream_t, int);
+                          int, int, int, int, int, float, void*, hipStream_t, int);
+size_t corr_workspace_bytes(int B, int OC, int Ho, int Wo);
 template <typename T>
 hipError_t corr_backward_t(const void*, const void*, const void*, void*, void*, int, int, int,
                            int, int, int, int, int, int, int, int, int, float, hipStream_t,
@@ -76,7 +77,7 @@ int force_generic() {
 
 extern "C" {
 
-int pwc_abi_version(void) { return 1; }
+int pwc_abi_version(void) { return 2; }
 
 const char* pwc_last_error(void) { return g_err; }
 
@@ -93,11 +94,10 @@ int pwc_corr_output_shape(int H, int W, int pad_size, int kernel_size, int max_d
   return 1;
 }
 
-int pwc_corr_forward(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
-                     int pad_size, int kernel_size, int max_displacement, int stride1,
-                     int stride2, int corr_multiply, int dtype, void* stream) {
-  (void)corr_multiply;  // ignored by the reference kernels as well
-  const char* fn = "pwc_corr_forward";
+static int corr_forward_impl(const char* fn, const void* in1, const void* in2, void* out, int B,
+                             int C, int H, int W, int pad_size, int kernel_size,
+                             int max_displacement, int stride1, int stride2, int dtype,
+                             void* workspace, size_t workspace_bytes, void* stream) {
   int OC, Ho, Wo;
   if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
   if (!corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
@@ -105,6 +105,8 @@ int pwc_corr_forward(const void* in1, const void* in2, void* out, int B, int C, 
     return fail(fn, "invalid correlation parameters");
   if (Ho <= 0 || Wo <= 0) return fail(fn, "empty correlation output");
   if ((size_t)B * C * H * W && (!in1 || !in2 || !out)) return fail(fn, "null buffer");
+  if (workspace && workspace_bytes < pwc::corr_workspace_bytes(B, OC, Ho, Wo))
+    return fail(fn, "workspace smaller than pwc_corr_workspace_size()");
   const float divisor = (float)(kernel_size * kernel_size * C);  // cu:65 nelems
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
@@ -112,22 +114,54 @@ int pwc_corr_forward(const void* in1, const void* in2, void* out, int B, int C, 
     case PWC_DTYPE_F32:
       e = pwc::corr_forward_t<float>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size, kernel_size,
                                      max_displacement, stride1, stride2, pwc::kRaster, divisor,
-                                     s, force_generic());
+                                     workspace, s, force_generic());
       break;
     case PWC_DTYPE_F16:
       e = pwc::corr_forward_t<__half>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size, kernel_size,
                                       max_displacement, stride1, stride2, pwc::kRaster,
-                                      divisor, s, force_generic());
+                                      divisor, workspace, s, force_generic());
       break;
     case PWC_DTYPE_BF16:
       e = pwc::corr_forward_t<__hip_bfloat16>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size,
                                               kernel_size, max_displacement, stride1, stride2,
-                                              pwc::kRaster, divisor, s, force_generic());
+                                              pwc::kRaster, divisor, workspace, s,
+                                              force_generic());
       break;
     default:
       return fail(fn, "unsupported dtype");
   }
   return check_launch(fn, e);
+}
+
+size_t pwc_corr_workspace_size(int B, int C, int H, int W, int pad_size, int kernel_size,
+                               int max_displacement, int stride1, int stride2) {
+  int OC, Ho, Wo;
+  (void)C;
+  if (!dims_ok(B, C, H, W) ||
+      !corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo) ||
+      Ho <= 0 || Wo <= 0)
+    return 0;
+  return pwc::corr_workspace_bytes(B, OC, Ho, Wo);
+}
+
+int pwc_corr_forward(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
+                     int pad_size, int kernel_size, int max_displacement, int stride1,
+                     int stride2, int corr_multiply, int dtype, void* stream) {
+  (void)corr_multiply;  // ignored by the reference kernels as well
+  return corr_forward_impl("pwc_corr_forward", in1, in2, out, B, C, H, W, pad_size,
+                           kernel_size, max_displacement, stride1, stride2, dtype, nullptr, 0,
+                           stream);
+}
+
+int pwc_corr_forward_ws(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
+                        int pad_size, int kernel_size, int max_displacement, int stride1,
+                        int stride2, int corr_multiply, int dtype, void* workspace,
+                        size_t workspace_bytes, void* stream) {
+  (void)corr_multiply;
+  return corr_forward_impl("pwc_corr_forward_ws", in1, in2, out, B, C, H, W, pad_size,
+                           kernel_size, max_displacement, stride1, stride2, dtype, workspace,
+                           workspace_bytes, stream);
 }
 
 int pwc_corr_backward(const void* in1, const void* in2, const void* grad_out, void* grad_in1,
@@ -172,13 +206,15 @@ int pwc_corr_backward(const void* in1, const void* in2, const void* grad_out, vo
   return check_launch(fn, e);
 }
 
-int pwc_cost_volume_forward(const void* src, const void* tgt, void* out, int B, int C, int H,
-                            int W, int search_range, int dtype, void* stream) {
-  const char* fn = "pwc_cost_volume_forward";
+static int cost_volume_forward_impl(const char* fn, const void* src, const void* tgt, void* out,
+                                    int B, int C, int H, int W, int search_range, int dtype,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
   if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
   if (search_range < 0) return fail(fn, "negative search_range");
   if ((size_t)B * C * H * W && (!src || !tgt || !out)) return fail(fn, "null buffer");
   const int K = (2 * search_range + 1) * (2 * search_range + 1);
+  if (workspace && workspace_bytes < pwc::corr_workspace_bytes(B, K, H, W))
+    return fail(fn, "workspace smaller than pwc_cost_volume_workspace_size()");
   const float divisor = (float)K;  // modules.py:74 output / shape[1]
   const int sr = search_range;
   hipStream_t s = (hipStream_t)stream;
@@ -187,20 +223,40 @@ int pwc_cost_volume_forward(const void* src, const void* tgt, void* out, int B, 
   switch (dtype) {
     case PWC_DTYPE_F32:
       e = pwc::corr_forward_t<float>(src, tgt, out, B, C, H, W, H, W, sr, 1, sr, 1, 1,
-                                     pwc::kCvl, divisor, s, force_generic());
+                                     pwc::kCvl, divisor, workspace, s, force_generic());
       break;
     case PWC_DTYPE_F16:
       e = pwc::corr_forward_t<__half>(src, tgt, out, B, C, H, W, H, W, sr, 1, sr, 1, 1,
-                                      pwc::kCvl, divisor, s, force_generic());
+                                      pwc::kCvl, divisor, workspace, s, force_generic());
       break;
     case PWC_DTYPE_BF16:
       e = pwc::corr_forward_t<__hip_bfloat16>(src, tgt, out, B, C, H, W, H, W, sr, 1, sr, 1, 1,
-                                              pwc::kCvl, divisor, s, force_generic());
+                                              pwc::kCvl, divisor, workspace, s,
+                                              force_generic());
       break;
     default:
       return fail(fn, "unsupported dtype");
   }
   return check_launch(fn, e);
+}
+
+size_t pwc_cost_volume_workspace_size(int B, int C, int H, int W, int search_range) {
+  if (!dims_ok(B, C, H, W) || search_range < 0) return 0;
+  const int K = (2 * search_range + 1) * (2 * search_range + 1);
+  return pwc::corr_workspace_bytes(B, K, H, W);
+}
+
+int pwc_cost_volume_forward(const void* src, const void* tgt, void* out, int B, int C, int H,
+                            int W, int search_range, int dtype, void* stream) {
+  return cost_volume_forward_impl("pwc_cost_volume_forward", src, tgt, out, B, C, H, W,
+                                  search_range, dtype, nullptr, 0, stream);
+}
+
+int pwc_cost_volume_forward_ws(const void* src, const void* tgt, void* out, int B, int C,
+                               int H, int W, int search_range, int dtype, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  return cost_volume_forward_impl("pwc_cost_volume_forward_ws", src, tgt, out, B, C, H, W,
+                                  search_range, dtype, workspace, workspace_bytes, stream);
 }
 
 int pwc_cost_volume_backward(const void* src, const void* tgt, const void* grad_out,

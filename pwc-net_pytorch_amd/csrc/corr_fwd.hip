@@ -18,9 +18,13 @@
 //   * blocks are remapped XCD-aware so neighbouring tiles (shared halo rows) share an L2.
 // Generic kernel: any (pad, k, md, s1, s2), one thread per output element; used for the
 // rarely-used configurations the tiled kernel does not instantiate.
+#include <cmath>
+
 #include "pwc_common.cuh"
 
 namespace pwc {
+
+constexpr int kMaxSplits = 16;  // channel splits per tile (workspace budget)
 
 template <int DR_, int S_, int GS_, int PX_, int NQ_, int TY_, int CC_>
 struct CorrTile {
@@ -91,7 +95,8 @@ struct Stager {
     return make_float4(e[0], e[1], e[2], e[3]);
   }
 
-  // Issue the global loads of chunk c0 (channels c0 .. c0+CC-1) into registers.
+  // Issue the global loads of chunk c0 (channels c0 .. c0+CC-1, those >= C read as zero) into
+  // registers.
   __device__ __forceinline__ void load(const T* __restrict__ f1n, const T* __restrict__ f2n,
                                        int c0, int C, int H, int W, int y1, int x1,
                                        bool vec_ok) {
@@ -159,11 +164,13 @@ struct Stager {
   }
 };
 
+// blockIdx.y = channel split k: channels [k*cps, min(C,(k+1)*cps)); with gridDim.y > 1 the raw
+// sums go to partial[k][n][oc][oy][ox] (fp32) for corr_reduce_splits.
 template <class G, typename T>
 __global__ __launch_bounds__(G::THREADS) void corr_fwd_tiled(
     const T* __restrict__ in1, const T* __restrict__ in2, T* __restrict__ out, int B, int C,
     int H, int W, int Ho, int Wo, int off, int layout, float divisor, int n_ty, int n_tx,
-    int vec_ok_i) {
+    int vec_ok_i, int cps, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const bool vec_ok = vec_ok_i != 0;
 
@@ -193,8 +200,10 @@ __global__ __launch_bounds__(G::THREADS) void corr_fwd_tiled(
     for (int k = 0; k < G::PX; ++k) acc[a][k] = 0.f;
 
   Stager<G, T> st;
-  const int nchunks = (C + G::CC - 1) / G::CC;
-  st.load(f1n, f2n, 0, C, H, W, y1, x1, vec_ok);
+  const int c_begin = blockIdx.y * cps;
+  const int c_end = min(C, c_begin + cps);
+  const int nchunks = (c_end - c_begin + G::CC - 1) / G::CC;
+  st.load(f1n, f2n, c_begin, c_end, H, W, y1, x1, vec_ok);
   st.store(lds);
   __syncthreads();
 
@@ -205,7 +214,8 @@ __global__ __launch_bounds__(G::THREADS) void corr_fwd_tiled(
 
   for (int ch = 0; ch < nchunks; ++ch) {
     const float* buf = lds + (ch & 1) * G::BUF_FLOATS;
-    if (ch + 1 < nchunks) st.load(f1n, f2n, (ch + 1) * G::CC, C, H, W, y1, x1, vec_ok);
+    if (ch + 1 < nchunks)
+      st.load(f1n, f2n, c_begin + (ch + 1) * G::CC, c_end, H, W, y1, x1, vec_ok);
 #pragma unroll
     for (int cc = 0; cc < G::CC; ++cc) {
       const float* F2 = buf + cc * G::R2 * G::RS2 + f2_off;
@@ -238,6 +248,20 @@ __global__ __launch_bounds__(G::THREADS) void corr_fwd_tiled(
   if (oy >= Ho) return;
   const int OC = G::D * G::D;
   const int tj = tjx - G::DR;
+  if (gridDim.y > 1) {
+    float* pk = partial + (size_t)blockIdx.y * B * OC * Ho * Wo;
+#pragma unroll
+    for (int ti = 0; ti < G::D; ++ti) {
+      const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
+      float* prow = pk + (((size_t)n * OC + oc) * Ho + oy) * Wo;
+#pragma unroll
+      for (int k = 0; k < G::PX; ++k) {
+        const int ox = ox0 + q * G::GS * G::PX + p + G::GS * k;
+        if (ox < Wo) prow[ox] = acc[ti][k];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int ti = 0; ti < G::D; ++ti) {
     const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
@@ -292,6 +316,47 @@ __global__ void corr_fwd_generic(const T* __restrict__ in1, const T* __restrict_
   }
 }
 
+// Split-channel reduction: out[i] = (sum_k partial[k][i]) / divisor, k ascending (fixed order,
+// deterministic).  inv_divisor != 0 when the divisor is a power of two (exact scale).
+template <typename T>
+__global__ __launch_bounds__(256) void corr_reduce_splits(const float* __restrict__ partial,
+                                                          T* __restrict__ out, size_t n,
+                                                          int nsplit, float divisor,
+                                                          float inv_divisor) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += partial[(size_t)k * n + i];
+    out[i] = from_f32<T>(inv_divisor != 0.f ? s * inv_divisor : s / divisor);
+  }
+}
+
+static float exact_inverse(float divisor) {
+  int ex;
+  const float m = std::frexp(divisor, &ex);
+  return (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
+}
+
+template <typename T>
+static hipError_t corr_reduce_splits_t(const void* partial, void* out, size_t n, int nsplit,
+                                       float divisor, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  size_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(corr_reduce_splits<T>, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     (const float*)partial, (T*)out, n, nsplit, divisor,
+                     exact_inverse(divisor));
+  return hipGetLastError();
+}
+
+hipError_t corr_reduce_splits_f32(const void* partial, void* out, size_t n, int nsplit,
+                                  float divisor, float inv_divisor, hipStream_t stream) {
+  (void)inv_divisor;
+  return corr_reduce_splits_t<float>(partial, out, n, nsplit, divisor, stream);
+}
+
+int corr_pick_splits(long long base_blocks, int nchunks, int max_splits);  // corr_ring.hip
+
 // ------------------------------------------------------------------------------------
 // host-side launchers
 // ------------------------------------------------------------------------------------
@@ -301,7 +366,8 @@ using Corr4 = CorrTile</*DR*/ 4, /*S*/ 1, /*GS*/ 1, /*PX*/ 4, /*NQ*/ 4, /*TY*/ 1
 template <class G, typename T>
 static hipError_t launch_tiled(const void* in1, const void* in2, void* out, int B, int C,
                                int H, int W, int Ho, int Wo, int off, int layout,
-                               float divisor, hipStream_t stream) {
+                               float divisor, int max_splits, void* partial,
+                               hipStream_t stream) {
   const int n_ty = (Ho + G::TY - 1) / G::TY;
   const int n_tx = (Wo + G::TX - 1) / G::TX;
   const long long nblk = (long long)B * n_ty * n_tx;
@@ -320,10 +386,18 @@ static hipError_t launch_tiled(const void* in1, const void* in2, void* out, int 
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((corr_fwd_tiled<G, T>), dim3((unsigned)nblk), dim3(G::THREADS),
-                     G::LDS_BYTES, stream, (const T*)in1, (const T*)in2, (T*)out, B, C, H, W,
-                     Ho, Wo, off, layout, divisor, n_ty, n_tx, vec_ok ? 1 : 0);
-  return hipGetLastError();
+  const int nchunks = (C + G::CC - 1) / G::CC;
+  int nsplit = partial ? corr_pick_splits(nblk, nchunks, max_splits) : 1;
+  const int cps = ((nchunks + nsplit - 1) / nsplit) * G::CC;
+  nsplit = C > 0 ? (C + cps - 1) / cps : 1;
+  hipLaunchKernelGGL((corr_fwd_tiled<G, T>), dim3((unsigned)nblk, (unsigned)nsplit),
+                     dim3(G::THREADS), G::LDS_BYTES, stream, (const T*)in1, (const T*)in2,
+                     (T*)out, B, C, H, W, Ho, Wo, off, layout, divisor, n_ty, n_tx,
+                     vec_ok ? 1 : 0, cps, (float*)partial);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nsplit == 1) return e;
+  return corr_reduce_splits_t<T>(partial, out, (size_t)B * G::D * G::D * Ho * Wo, nsplit,
+                                 divisor, stream);
 }
 
 template <typename T>
@@ -346,40 +420,65 @@ static hipError_t launch_generic(const void* in1, const void* in2, void* out, in
 // corr_ring.hip
 hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, int B, int C,
                                  int H, int W, int Ho, int Wo, int off, int dr, int s2,
-                                 int layout, float divisor, hipStream_t stream);
+                                 int layout, float divisor, int max_splits, void* partial,
+                                 hipStream_t stream);
 
+// Channel-split budget: nsplit partial volumes of B*OC*Ho*Wo floats, nsplit <= kMaxSplits and
+// nsplit * volume <= kSplitBudget; no workspace once the 16x16 tiles alone fill the chip.
+constexpr size_t kSplitBudget = 16u << 20;
+
+int corr_max_splits(int B, int OC, int Ho, int Wo) {
+  const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
+  const size_t vol = (size_t)B * OC * Ho * Wo * sizeof(float);
+  if (tiles >= 256 || vol == 0) return 1;
+  size_t k = kSplitBudget / vol;
+  if (k > (size_t)kMaxSplits) k = kMaxSplits;
+  return k < 2 ? 1 : (int)k;
+}
+
+size_t corr_workspace_bytes(int B, int OC, int Ho, int Wo) {
+  const int k = corr_max_splits(B, OC, Ho, Wo);
+  return k > 1 ? (size_t)k * B * OC * Ho * Wo * sizeof(float) : 0;
+}
+
+// `workspace` (>= corr_workspace_bytes) enables channel splitting for grids too small to fill
+// the chip; null keeps one workgroup per tile over all channels.
 template <typename T>
 hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, int C, int H,
                           int W, int Ho, int Wo, int pad, int k, int md, int s1, int s2,
-                          int layout, float divisor, hipStream_t stream, int force_generic) {
+                          int layout, float divisor, void* workspace, hipStream_t stream,
+                          int force_generic) {
   const int kr = (k - 1) / 2;
   const int dr = md / s2;
+  const int D = 2 * dr + 1;
+  const int max_splits = workspace ? corr_max_splits(B, D * D, Ho, Wo) : 1;
+  if (max_splits <= 1) workspace = nullptr;
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4) {
     const hipError_t e = corr_forward_ring_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad, dr,
-                                               s2, layout, divisor, stream);
+                                               s2, layout, divisor, max_splits, workspace,
+                                               stream);
     if (e != hipErrorNotSupported) return e;
   }
   if (force_generic != 1 && k == 1 && s1 == 1 && dr == 4) {
     const int off = md - pad;
     if (s2 == 2)
       return launch_tiled<Corr9, T>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor,
-                                    stream);
+                                    max_splits, workspace, stream);
     if (s2 == 1)
       return launch_tiled<Corr4, T>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor,
-                                    stream);
+                                    max_splits, workspace, stream);
   }
   return launch_generic<T>(in1, in2, out, B, C, H, W, Ho, Wo, pad, kr, md, s1, s2, dr, layout,
                            divisor, stream);
 }
 
-template hipError_t corr_forward_t<float>(const void*, const void*, void*, int, int, int, int,
-                                          int, int, int, int, int, int, int, int, float,
-                                          hipStream_t, int);
-template hipError_t corr_forward_t<__half>(const void*, const void*, void*, int, int, int, int,
-                                           int, int, int, int, int, int, int, int, float,
-                                           hipStream_t, int);
-template hipError_t corr_forward_t<__hip_bfloat16>(const void*, const void*, void*, int, int,
-                                                   int, int, int, int, int, int, int, int, int,
-                                                   int, float, hipStream_t, int);
+#define PWC_INST(T)                                                                          \
+  template hipError_t corr_forward_t<T>(const void*, const void*, void*, int, int, int, int,   \
+                                        int, int, int, int, int, int, int, int, float, void*,  \
+                                        hipStream_t, int);
+PWC_INST(float)
+PWC_INST(__half)
+PWC_INST(__hip_bfloat16)
+#undef PWC_INST
 
 }  // namespace pwc

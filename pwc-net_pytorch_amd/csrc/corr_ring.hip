@@ -29,6 +29,10 @@
 
 namespace pwc {
 
+// corr_fwd.hip: out[i] = (sum_k partial[k][i]) / divisor, k in order (deterministic).
+hipError_t corr_reduce_splits_f32(const void* partial, void* out, size_t n, int nsplit,
+                                  float divisor, float inv_divisor, hipStream_t stream);
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int N>
@@ -87,7 +91,8 @@ struct RingTile {
 };
 
 template <class G>
-__device__ __forceinline__ void ring_issue(int stage, int wave, uint32_t plane, uint32_t lds0,
+__device__ __forceinline__ void ring_issue(int stage, int c_begin, int wave, uint32_t plane,
+                                           uint32_t lds0,
                                            __amdgpu_buffer_rsrc_t rs1,
                                            __amdgpu_buffer_rsrc_t rs2,
                                            const uint32_t (&src_off)[G::PPW],
@@ -95,7 +100,7 @@ __device__ __forceinline__ void ring_issue(int stage, int wave, uint32_t plane, 
                                            const bool (&from_f2)[G::PPW]) {
   constexpr uint32_t kOOB = 0x80000000u;
   if (wave >= G::ISSUERS) return;
-  const uint32_t cbytes = (uint32_t)(stage * G::CC) * plane * 4u;  // channel advance
+  const uint32_t cbytes = (uint32_t)(c_begin + stage * G::CC) * plane * 4u;  // channel advance
   const uint32_t sbase = lds0 + (uint32_t)((stage % G::NS) * G::STAGE_FLOATS) * 4u;
 #pragma unroll
   for (int i = 0; i < G::PPW; ++i) {
@@ -108,12 +113,22 @@ __device__ __forceinline__ void ring_issue(int stage, int wave, uint32_t plane, 
   }
 }
 
+// Channel split (blockIdx.y = split k of nsplit): split k sums channels
+// [k*cps, min(C, (k+1)*cps)) and, when nsplit > 1, stores its raw sums to
+// partial[k][n][oc][oy][ox] for corr_reduce_splits (fixed-order, deterministic).
 template <class G>
-__global__ __launch_bounds__(G::THREADS, 5) void corr_fwd_ring(
+__global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
     int C, int H, int W, int Ho, int Wo, int off, int layout, float divisor, float inv_divisor,
-    int n_ty, int n_tx) {
+    int n_ty, int n_tx, int cps, float* __restrict__ partial
+#ifdef PWC_RING_CENSUS
+    , unsigned* census
+#endif
+    ) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+#ifdef PWC_RING_CENSUS  // diagnostic build only (tools/occupancy.hip): residency census
+  unsigned long long census_t0 = __builtin_amdgcn_s_memtime();
+#endif
 
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int tx_tile = t % n_tx;
@@ -181,10 +196,13 @@ __global__ __launch_bounds__(G::THREADS, 5) void corr_fwd_ring(
 #pragma unroll
     for (int k = 0; k < G::PX; ++k) acc[a][k] = 0.f;
 
-  const int nst = (C + G::CC - 1) / G::CC;
+  const int c_begin = blockIdx.y * cps;
+  const int c_end = min(C, c_begin + cps);
+  const int nst = (c_end - c_begin + G::CC - 1) / G::CC;  // cps is a multiple of CC
 #pragma unroll
   for (int s = 0; s < G::NS - 1; ++s)
-    if (s < nst) ring_issue<G>(s, wave, plane, lds0, rs1, rs2, src_off, dst_off, from_f2);
+    if (s < nst)
+      ring_issue<G>(s, c_begin, wave, plane, lds0, rs1, rs2, src_off, dst_off, from_f2);
 
   for (int st = 0; st < nst; ++st) {
     if (wave < G::ISSUERS) {
@@ -195,7 +213,8 @@ __global__ __launch_bounds__(G::THREADS, 5) void corr_fwd_ring(
     }
     __builtin_amdgcn_s_barrier();
     if (st + G::NS - 1 < nst)
-      ring_issue<G>(st + G::NS - 1, wave, plane, lds0, rs1, rs2, src_off, dst_off, from_f2);
+      ring_issue<G>(st + G::NS - 1, c_begin, wave, plane, lds0, rs1, rs2, src_off, dst_off,
+                    from_f2);
     const uint32_t sb = lds0 + (uint32_t)((st % G::NS) * G::STAGE_FLOATS) * 4u;
 #pragma unroll 1  // one channel's operands live at a time: 96 VGPRs, 2 workgroups/CU
     for (int cc = 0; cc < G::CC; ++cc) {
@@ -219,12 +238,34 @@ __global__ __launch_bounds__(G::THREADS, 5) void corr_fwd_ring(
     }
   }
 
+#ifdef PWC_RING_CENSUS
+  if (threadIdx.x == 0) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    census[blockIdx.x * 4 + 0] = hw;
+    census[blockIdx.x * 4 + 1] = xcc;
+    census[blockIdx.x * 4 + 2] = (unsigned)census_t0;
+    census[blockIdx.x * 4 + 3] = (unsigned)__builtin_amdgcn_s_memtime();
+  }
+#endif
   // ---- epilogue: out = acc / divisor (cu:100); a power-of-two divisor is an exact scale ----
   const int oy = oy0 + ty;
   const int ox = ox0 + 4 * q;
   if (oy >= Ho || ox >= Wo) return;
   const int OC = G::D * G::D;
   const int tj = tjx - G::DR;
+  if (gridDim.y > 1) {  // split: raw partial sums, reduced by corr_reduce_splits
+    float* pk = partial + (size_t)blockIdx.y * ((size_t)gridDim.x / (n_tx * n_ty)) * OC * Ho * Wo;
+#pragma unroll
+    for (int ti = 0; ti < G::D; ++ti) {
+      const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
+      float* orow = pk + (((size_t)n * OC + oc) * Ho + oy) * Wo;
+      *reinterpret_cast<float4*>(orow + ox) =
+          make_float4(acc[ti][0], acc[ti][1], acc[ti][2], acc[ti][3]);
+    }
+    return;
+  }
   const bool pow2 = inv_divisor != 0.f;
 #pragma unroll
   for (int ti = 0; ti < G::D; ++ti) {
@@ -251,10 +292,14 @@ using RingC = RingTile<4, 2, 16, 2, 6, 2>;  // 60 KiB, 5 in flight
 using RingD = RingTile<4, 2, 16, 3, 5, 3>;  // 75 KiB, 4 in flight
 using RingE = RingTile<4, 2, 16, 2, 8, 2>;  // 80 KiB, 7 in flight
 
+#ifdef PWC_RING_CENSUS
+unsigned* g_census = nullptr;
+#endif
+
 template <class G>
 static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B, int C, int H,
                               int W, int Ho, int Wo, int off, int layout, float divisor,
-                              hipStream_t stream) {
+                              int nsplit, void* partial, hipStream_t stream) {
   const int n_ty = (Ho + G::TY - 1) / G::TY;
   const int n_tx = (Wo + G::TX - 1) / G::TX;
   const long long nblk = (long long)B * n_ty * n_tx;
@@ -268,41 +313,70 @@ static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  const int nchunks = (C + G::CC - 1) / G::CC;
+  if (nsplit > nchunks) nsplit = nchunks;
+  if (nsplit < 1) nsplit = 1;
+  const int cps = ((nchunks + nsplit - 1) / nsplit) * G::CC;
+  nsplit = (C + cps - 1) / cps;
   // exact reciprocal when the divisor is a power of two (then x * inv == x / divisor)
   int ex;
   const float m = std::frexp(divisor, &ex);
   const float inv = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
-  hipLaunchKernelGGL((corr_fwd_ring<G>), dim3((unsigned)nblk), dim3(G::THREADS), G::LDS_BYTES,
-                     stream, (const float*)in1, (const float*)in2, (float*)out, C, H, W, Ho,
-                     Wo, off, layout, divisor, inv, n_ty, n_tx);
-  return hipGetLastError();
+  hipLaunchKernelGGL((corr_fwd_ring<G>), dim3((unsigned)nblk, (unsigned)nsplit),
+                     dim3(G::THREADS), G::LDS_BYTES, stream, (const float*)in1,
+                     (const float*)in2, (float*)out, C, H, W, Ho, Wo, off, layout, divisor, inv,
+                     n_ty, n_tx, cps, (float*)partial
+#ifdef PWC_RING_CENSUS
+                     , g_census
+#endif
+                     );
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nsplit == 1) return e;
+  return corr_reduce_splits_f32(partial, out, (size_t)B * G::D * G::D * Ho * Wo, nsplit,
+                                divisor, inv, stream);
 }
 
 static int ring_cfg() {
   static int v = -1;
   if (v < 0) {
     const char* s = std::getenv("PWC_RING_CFG");
-    v = 1;  // default: B
+    v = 2;  // default: C
     if (s && s[0] >= 'A' && s[0] <= 'E' && s[1] == 0) v = s[0] - 'A';
   }
   return v;
 }
 
+// Number of channel splits for a grid of `base_blocks` tiles: none once the tiles alone give
+// every CU a workgroup; otherwise aim at two workgroups per CU (512), at most one split per
+// channel chunk and at most `max_splits` (the caller sizes max_splits so that the partial
+// volumes stay within the workspace budget, corr_workspace_bytes).
+int corr_pick_splits(long long base_blocks, int nchunks, int max_splits) {
+  if (base_blocks <= 0 || base_blocks >= 256) return 1;
+  long long k = (512 + base_blocks - 1) / base_blocks;
+  if (k > nchunks) k = nchunks;
+  if (k > max_splits) k = max_splits;
+  return k < 1 ? 1 : (int)k;
+}
+
 // hipErrorNotSupported: shape / alignment outside what the ring kernel handles.
+// `partial` (nsplit * B*81*Ho*Wo floats) may be null when nsplit == 1.
 hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, int B, int C,
                                  int H, int W, int Ho, int Wo, int off, int dr, int s2,
-                                 int layout, float divisor, hipStream_t stream) {
+                                 int layout, float divisor, int max_splits, void* partial,
+                                 hipStream_t stream) {
   if (!(dr == 4 && s2 == 2)) return hipErrorNotSupported;
   if (W % 4 || Wo % 4 || off % 4) return hipErrorNotSupported;
   if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16)
     return hipErrorNotSupported;
   if ((size_t)C * H * W * 4 >= 0x7ffffff0ull) return hipErrorNotSupported;
+  const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
+  const int ns = partial ? corr_pick_splits(tiles, (C + 3) / 4, max_splits) : 1;
   switch (ring_cfg()) {
-    case 0: return launch_ring<RingA>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
-    case 2: return launch_ring<RingC>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
-    case 3: return launch_ring<RingD>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
-    case 4: return launch_ring<RingE>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
-    default: return launch_ring<RingB>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    case 0: return launch_ring<RingA>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 1: return launch_ring<RingB>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 3: return launch_ring<RingD>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 4: return launch_ring<RingE>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    default: return launch_ring<RingC>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
   }
 }
 

@@ -24,19 +24,24 @@ DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
 # Every symbol the header declares: (name, restype, argtypes).
 _P = ctypes.c_void_p
 _I = ctypes.c_int
+_Z = ctypes.c_size_t
 _IP = ctypes.POINTER(ctypes.c_int)
 SYMBOLS = {
     "pwc_abi_version": (_I, []),
     "pwc_last_error": (ctypes.c_char_p, []),
     "pwc_corr_output_shape": (_I, [_I] * 7 + [_IP] * 3),
     "pwc_corr_forward": (_I, [_P, _P, _P] + [_I] * 11 + [_P]),
+    "pwc_corr_workspace_size": (_Z, [_I] * 9),
+    "pwc_corr_forward_ws": (_I, [_P, _P, _P] + [_I] * 11 + [_P, _Z, _P]),
     "pwc_corr_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 11 + [_P]),
     "pwc_cost_volume_forward": (_I, [_P, _P, _P] + [_I] * 6 + [_P]),
+    "pwc_cost_volume_workspace_size": (_Z, [_I] * 5),
+    "pwc_cost_volume_forward_ws": (_I, [_P, _P, _P] + [_I] * 6 + [_P, _Z, _P]),
     "pwc_cost_volume_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 6 + [_P]),
     "pwc_warp_forward": (_I, [_P, _P, _P] + [_I] * 5 + [_P]),
     "pwc_warp_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 5 + [_P]),
 }
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lock = threading.Lock()
 _lib = None

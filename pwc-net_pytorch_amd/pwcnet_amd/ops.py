@@ -42,6 +42,14 @@ def _check_inputs(what: str, *ts: torch.Tensor, dtypes=tuple(_lib.DTYPE_CODES)) 
             raise ValueError(f"{what}: expected NCHW 4-d tensors, got shape {tuple(t.shape)}")
 
 
+def _workspace(nbytes: int, device):
+    """Split-channel scratch from the caching allocator (stream-ordered, graph-capturable)."""
+    if nbytes == 0:
+        return None, ctypes.c_void_p(0)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    return ws, ctypes.c_void_p(ws.data_ptr())
+
+
 def _i32(*vals) -> None:
     for v in vals:
         if not (-(2 ** 31) <= int(v) < 2 ** 31):
@@ -64,10 +72,15 @@ def corr_forward(input1, input2, pad_size, kernel_size, max_displacement, stride
     out = torch.empty((B, OC, Ho, Wo), dtype=input1.dtype, device=input1.device)
     if out.numel() == 0:
         return out
-    _lib.check(_lib.load().pwc_corr_forward(
+    lib = _lib.load()
+    nws = lib.pwc_corr_workspace_size(B, C, H, W, pad_size, kernel_size, max_displacement,
+                                      stride1, stride2)
+    ws, wsp = _workspace(nws, input1.device)
+    _lib.check(lib.pwc_corr_forward_ws(
         _ptr(input1), _ptr(input2), _ptr(out), B, C, H, W, pad_size, kernel_size,
         max_displacement, stride1, stride2, corr_multiply, _lib.DTYPE_CODES[input1.dtype],
-        _stream(input1.device)), "Correlation_forward")
+        wsp, nws, _stream(input1.device)), "Correlation_forward")
+    del ws  # the caching allocator keeps it stream-ordered until the kernels ran
     return out
 
 
@@ -135,9 +148,13 @@ def cost_volume_forward(src, tgt, search_range):
     out = torch.empty((B, K, H, W), dtype=src.dtype, device=src.device)
     if out.numel() == 0:
         return out
-    _lib.check(_lib.load().pwc_cost_volume_forward(
+    lib = _lib.load()
+    nws = lib.pwc_cost_volume_workspace_size(B, C, H, W, search_range)
+    ws, wsp = _workspace(nws, src.device)
+    _lib.check(lib.pwc_cost_volume_forward_ws(
         _ptr(src), _ptr(tgt), _ptr(out), B, C, H, W, search_range, _lib.DTYPE_CODES[src.dtype],
-        _stream(src.device)), "CostVolumeLayer_forward")
+        wsp, nws, _stream(src.device)), "CostVolumeLayer_forward")
+    del ws
     return out
 
 

@@ -242,3 +242,44 @@ def test_layers_reject_cpu_tensors():
     from pwcnet_amd.ops import corr_forward
     with pytest.raises(RuntimeError):
         corr_forward(torch.zeros(1, 2, 3, 3), torch.zeros(1, 2, 3, 3), 9, 1, 9, 1, 2)
+
+
+@pytest.mark.parametrize("case", [(1, 192, 6, 7), (2, 128, 12, 14), (2, 96, 24, 28),
+                                  (1, 64, 48, 56)])
+def test_corr_forward_with_and_without_workspace(case):
+    """pwc_corr_forward (single pass over C) and pwc_corr_forward_ws (channel split into a
+    caller workspace + fixed-order reduce) both match the oracle; the split result is
+    deterministic across calls."""
+    import ctypes
+    from pwcnet_amd import _lib
+    B, C, H, W = case
+    rng = np.random.default_rng(21)
+    a, b = _t(_rand(rng, B, C, H, W)), _t(_rand(rng, B, C, H, W))
+    lib = _lib.load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ref = O.corr_forward(_np(a), _np(b), 9, 1, 9, 1, 2)
+    out0 = torch.empty(B, 81, H, W, device=DEV)
+    _lib.check(lib.pwc_corr_forward(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                                    ctypes.c_void_p(out0.data_ptr()), B, C, H, W, 9, 1, 9, 1, 2,
+                                    1, 0, stream), "t")
+    nws = lib.pwc_corr_workspace_size(B, C, H, W, 9, 1, 9, 1, 2)
+    assert nws > 0  # these grids are small enough to split
+    ws = torch.empty(nws, dtype=torch.uint8, device=DEV)
+    outs = []
+    for _ in range(2):
+        o = torch.empty(B, 81, H, W, device=DEV)
+        _lib.check(lib.pwc_corr_forward_ws(
+            ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+            ctypes.c_void_p(o.data_ptr()), B, C, H, W, 9, 1, 9, 1, 2, 1, 0,
+            ctypes.c_void_p(ws.data_ptr()), nws, stream), "t")
+        outs.append(o)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(out0), ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_np(outs[0]), ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(outs[0], outs[1])
+    # undersized workspace is an error, not a silent fallback
+    with pytest.raises(RuntimeError, match="workspace"):
+        _lib.check(lib.pwc_corr_forward_ws(
+            ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+            ctypes.c_void_p(outs[0].data_ptr()), B, C, H, W, 9, 1, 9, 1, 2, 1, 0,
+            ctypes.c_void_p(ws.data_ptr()), nws - 4, stream), "t")
