@@ -44,21 +44,54 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-// Six ds_read_b128 + lgkmcnt(0) in one statement (see file header).
+// Six ds_read_b128 + lgkmcnt(0) in one statement (see file header).  OFF is the channel's
+// byte offset inside the stage, folded into the instructions' 16-bit offset field so the
+// per-channel address arithmetic disappears.
+template <int OFF>
 __device__ __forceinline__ void lds_read6(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
                                           uint32_t a4, uint32_t a5, f32x4& r0, f32x4& r1,
                                           f32x4& r2, f32x4& r3, f32x4& r4, f32x4& r5) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
   asm volatile(
-      "ds_read_b128 %0, %6\n\t"
-      "ds_read_b128 %1, %7\n\t"
-      "ds_read_b128 %2, %8\n\t"
-      "ds_read_b128 %3, %9\n\t"
-      "ds_read_b128 %4, %10\n\t"
-      "ds_read_b128 %5, %11\n\t"
+      "ds_read_b128 %0, %6 offset:%12\n\t"
+      "ds_read_b128 %1, %7 offset:%12\n\t"
+      "ds_read_b128 %2, %8 offset:%12\n\t"
+      "ds_read_b128 %3, %9 offset:%12\n\t"
+      "ds_read_b128 %4, %10 offset:%12\n\t"
+      "ds_read_b128 %5, %11 offset:%12\n\t"
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5)
-      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "n"(OFF)
       : "memory");
+}
+
+// One channel of one stage: 6 LDS quads in, 36 FMAs (4 pixels x 9 ti) out.
+template <class G, int CC_I>
+__device__ __forceinline__ void ring_channel(const uint32_t (&addr)[6], float (&acc)[G::D][G::PX]) {
+  f32x4 a4, b[G::NWQ];
+  lds_read6<CC_I * G::CH_FLOATS * 4>(addr[0], addr[1], addr[2], addr[3], addr[4], addr[5], a4,
+                                     b[0], b[1], b[2], b[3], b[4]);
+  const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+  float w[4 * G::NWQ];
+#pragma unroll
+  for (int u = 0; u < G::NWQ; ++u) {
+    w[4 * u + 0] = b[u].x;
+    w[4 * u + 1] = b[u].y;
+    w[4 * u + 2] = b[u].z;
+    w[4 * u + 3] = b[u].w;
+  }
+#pragma unroll
+  for (int ti = 0; ti < G::D; ++ti)
+#pragma unroll
+    for (int k = 0; k < G::PX; ++k) acc[ti][k] = fmaf(av[k], w[k + G::S * ti], acc[ti][k]);
+}
+
+template <class G, int CC_I>
+__device__ __forceinline__ void ring_stage(const uint32_t (&addr)[6], float (&acc)[G::D][G::PX]) {
+  if constexpr (CC_I < G::CC) {
+    ring_channel<G, CC_I>(addr, acc);
+    ring_stage<G, CC_I + 1>(addr, acc);
+  }
 }
 
 template <int DR_, int S_, int TY_, int CC_, int NS_, int PPW_>
@@ -89,6 +122,10 @@ struct RingTile {
   static_assert(THREADS % 64 == 0 && THREADS <= 1024, "workgroup");
   static_assert(NS >= 2, "ring depth");
 };
+
+#ifdef PWC_RING_ABLATION
+__constant__ int g_ablation;
+#endif
 
 template <class G>
 __device__ __forceinline__ void ring_issue(int stage, int c_begin, int wave, uint32_t plane,
@@ -127,7 +164,7 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     ) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #ifdef PWC_RING_CENSUS  // diagnostic build only (tools/occupancy.hip): residency census
-  unsigned long long census_t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long census_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
 
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -212,30 +249,19 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
         wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
+#ifdef PWC_RING_ABLATION  // diagnostic build: g_ablation 1 = no FMA work, 2 = no DMA
+    if (g_ablation != 2)
+#endif
     if (st + G::NS - 1 < nst)
       ring_issue<G>(st + G::NS - 1, c_begin, wave, plane, lds0, rs1, rs2, src_off, dst_off,
                     from_f2);
     const uint32_t sb = lds0 + (uint32_t)((st % G::NS) * G::STAGE_FLOATS) * 4u;
-#pragma unroll 1  // one channel's operands live at a time: 96 VGPRs, 2 workgroups/CU
-    for (int cc = 0; cc < G::CC; ++cc) {
-      const uint32_t cb = sb + (uint32_t)(cc * G::CH_FLOATS) * 4u;
-      f32x4 a4, b[G::NWQ];
-      lds_read6(cb + aoff, cb + woff[0], cb + woff[1], cb + woff[2], cb + woff[3], cb + woff[4],
-                a4, b[0], b[1], b[2], b[3], b[4]);
-      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-      float w[4 * G::NWQ];
-#pragma unroll
-      for (int u = 0; u < G::NWQ; ++u) {
-        w[4 * u + 0] = b[u].x;
-        w[4 * u + 1] = b[u].y;
-        w[4 * u + 2] = b[u].z;
-        w[4 * u + 3] = b[u].w;
-      }
-#pragma unroll
-      for (int ti = 0; ti < G::D; ++ti)
-#pragma unroll
-        for (int k = 0; k < G::PX; ++k) acc[ti][k] = fmaf(av[k], w[k + G::S * ti], acc[ti][k]);
-    }
+#ifdef PWC_RING_ABLATION
+    if (g_ablation == 1) continue;
+#endif
+    const uint32_t addr[6] = {sb + aoff, sb + woff[0], sb + woff[1], sb + woff[2], sb + woff[3],
+                              sb + woff[4]};
+    ring_stage<G, 0>(addr, acc);
   }
 
 #ifdef PWC_RING_CENSUS
@@ -246,7 +272,7 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     census[blockIdx.x * 4 + 0] = hw;
     census[blockIdx.x * 4 + 1] = xcc;
     census[blockIdx.x * 4 + 2] = (unsigned)census_t0;
-    census[blockIdx.x * 4 + 3] = (unsigned)__builtin_amdgcn_s_memtime();
+    census[blockIdx.x * 4 + 3] = (unsigned)__builtin_amdgcn_s_memrealtime();
   }
 #endif
   // ---- epilogue: out = acc / divisor (cu:100); a power-of-two divisor is an exact scale ----

@@ -26,6 +26,13 @@ int main(int argc, char** argv) {
   report<RingB>("RingB");
   report<RingC>("RingC");
   const int B = argc > 1 ? atoi(argv[1]) : 7, C = 32, H = 96, W = 112;
+#ifdef PWC_RING_ABLATION
+  {
+    const int abl = argc > 2 ? atoi(argv[2]) : 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ablation), &abl, sizeof(int));
+    printf("ablation %d\n", abl);
+  }
+#endif
   size_t n = (size_t)B * C * H * W;
   float *a, *b, *o;
   (void)hipMalloc(&a, n * 4);
@@ -36,8 +43,21 @@ int main(int argc, char** argv) {
   const int nb = B * 6 * 7;
   (void)hipMalloc(&g_census, nb * 16);
   for (int rep = 0; rep < 3; ++rep)
-    (void)corr_forward_ring_f32(a, b, o, B, C, H, W, H, W, 0, 4, 2, 0, 32.f, 0);
+    (void)corr_forward_ring_f32(a, b, o, B, C, H, W, H, W, 0, 4, 2, 0, 32.f, 1, nullptr, 0);
   (void)hipDeviceSynchronize();
+  {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, 0);
+    for (int rep = 0; rep < 50; ++rep)
+      (void)corr_forward_ring_f32(a, b, o, B, C, H, W, H, W, 0, 4, 2, 0, 32.f, 1, nullptr, 0);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("  back-to-back: %.2f us per launch\n", ms * 1000 / 50);
+  }
   std::vector<unsigned> h(nb * 4);
   (void)hipMemcpy(h.data(), g_census, nb * 16, hipMemcpyDeviceToHost);
   int maxc = 0;
@@ -55,19 +75,17 @@ int main(int argc, char** argv) {
   }
   printf("ring B=%d (%d workgroups): max co-resident on one CU = %d, mean lifetime %.0f ticks\n",
          B, nb, maxc, life / nb);
-  for (unsigned x = 0; x < 8; ++x) {
-    unsigned lo = ~0u, hi = 0, first_end = ~0u, last_start = 0;
-    int cnt = 0;
-    for (int i = 0; i < nb; ++i)
-      if (h[i * 4 + 1] == x) {
-        ++cnt;
-        lo = std::min(lo, h[i * 4 + 2]);
-        hi = std::max(hi, h[i * 4 + 3]);
-        first_end = std::min(first_end, h[i * 4 + 3]);
-        last_start = std::max(last_start, h[i * 4 + 2]);
-      }
-    printf("  xcc %u: %d wg, span %u ticks, last start +%u, first end +%u\n", x, cnt, hi - lo,
-           last_start - lo, first_end - lo);
-  }
+  unsigned g0 = ~0u;
+  for (int i = 0; i < nb; ++i) g0 = std::min(g0, h[i * 4 + 2]);
+  std::vector<unsigned> st, en;
+  for (int i = 0; i < nb; ++i) { st.push_back(h[i * 4 + 2] - g0); en.push_back(h[i * 4 + 3] - g0); }
+  std::vector<unsigned> s2 = st, e2 = en;
+  std::sort(s2.begin(), s2.end());
+  std::sort(e2.begin(), e2.end());
+  printf("  (100 MHz ticks) start: min %u p50 %u p90 %u max %u | end: min %u p50 %u max %u\n",
+         s2[0], s2[nb / 2], s2[nb * 9 / 10], s2[nb - 1], e2[0], e2[nb / 2], e2[nb - 1]);
+  int late = 0;
+  for (int i = 0; i < nb; ++i) late += st[i] > 50;  // started > 0.5 us after the first block
+  printf("  blocks starting > 0.5 us late: %d of %d\n", late, nb);
   return 0;
 }
