@@ -139,6 +139,7 @@ def main():
 
     from pwcnet_amd import _lib
     from pwcnet_amd.ops import warp_forward, corr_forward
+    from pwcnet_amd.shard import max_over_ranks
     lib = _lib.load()
 
     dtype = torch.float32 if args.dtype == "fp32" else torch.float16
@@ -194,16 +195,18 @@ def main():
             w = warped[k]
         else:
             w = pre(sets[k])
-        if ev is not None:
-            ev[0].record(stream)
+        if ev is not None:  # kernel start/end events on this stream (hipExtLaunchKernel)
+            _lib.check(lib.pwc_time_next_corr(ctypes.c_void_p(ev[0].cuda_event),
+                                               ctypes.c_void_p(ev[1].cuda_event)), "bench")
         corr_l4(sets[k], w)
-        if ev is not None:
-            ev[1].record(stream)
 
     for i in range(args.warmup):
         step(i)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
+    for a, b in evs:  # materialise the hipEvent_t handles (torch creates them lazily)
+        a.record(stream)
+        b.record(stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -214,10 +217,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, device=dev)  # MAX over ranks (no-op at N=1)
 
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     pairs = B * args.steps * world

@@ -48,8 +48,14 @@ extern "C" {
 #define PWC_DTYPE_F16 1
 #define PWC_DTYPE_BF16 2
 
-/* ABI version; bumped on any signature change (2: workspace entry points). */
+/* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook). */
 PWC_API int pwc_abi_version(void);
+
+/* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
+ * LDS-DMA kernel is launched with hipExtLaunchKernel, recording `start_event` / `stop_event`
+ * (hipEvent_t, timing enabled) at that kernel's start and end on its stream.  One-shot; pass
+ * (NULL, NULL) to disarm.  Used by bench.py to time the dominant kernel live. */
+PWC_API int pwc_time_next_corr(void* start_event, void* stop_event);
 
 /* Last error message of the calling thread ("" if none). */
 PWC_API const char* pwc_last_error(void);

@@ -25,6 +25,15 @@ hipError_t warp_backward_f32(const void*, const void*, const void*, void*, void*
                              int, hipStream_t);
 }  // namespace pwc
 
+namespace pwc {
+thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
+void take_launch_events(hipEvent_t* start, hipEvent_t* stop) {
+  *start = g_ev_start;
+  *stop = g_ev_stop;
+  g_ev_start = g_ev_stop = nullptr;
+}
+}  // namespace pwc
+
 namespace {
 
 thread_local char g_err[512] = "";
@@ -77,7 +86,15 @@ int force_generic() {
 
 extern "C" {
 
-int pwc_abi_version(void) { return 2; }
+int pwc_abi_version(void) { return 3; }
+
+int pwc_time_next_corr(void* start_event, void* stop_event) {
+  if ((start_event == nullptr) != (stop_event == nullptr))
+    return fail("pwc_time_next_corr", "give both events or neither");
+  pwc::g_ev_start = (hipEvent_t)start_event;
+  pwc::g_ev_stop = (hipEvent_t)stop_event;
+  return 1;
+}
 
 const char* pwc_last_error(void) { return g_err; }
 

@@ -22,12 +22,17 @@
 //   * waves wait on their own DMA with a counted vmcnt and meet at a raw s_barrier (a
 //     __syncthreads() would drain every in-flight stage);
 //   * tiles are remapped XCD-aware so neighbouring tiles (shared halo rows) share an L2.
+#include <hip/hip_ext.h>
+
 #include <cstdlib>
 #include <cstring>
 
 #include "pwc_common.cuh"
 
 namespace pwc {
+
+// capi.hip: one-shot start/stop events for the next main correlation dispatch of this thread.
+void take_launch_events(hipEvent_t* start, hipEvent_t* stop);
 
 // corr_fwd.hip: out[i] = (sum_k partial[k][i]) / divisor, k in order (deterministic).
 hipError_t corr_reduce_splits_f32(const void* partial, void* out, size_t n, int nsplit,
@@ -348,14 +353,18 @@ static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B
   int ex;
   const float m = std::frexp(divisor, &ex);
   const float inv = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
-  hipLaunchKernelGGL((corr_fwd_ring<G>), dim3((unsigned)nblk, (unsigned)nsplit),
-                     dim3(G::THREADS), G::LDS_BYTES, stream, (const float*)in1,
-                     (const float*)in2, (float*)out, C, H, W, Ho, Wo, off, layout, divisor, inv,
-                     n_ty, n_tx, cps, (float*)partial
+  // Optional kernel-start/-end events armed by pwc_time_next_corr (bench.py's live roofline
+  // timing: the events bracket exactly this dispatch on `stream`).
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  take_launch_events(&ev0, &ev1);
+  hipExtLaunchKernelGGL((corr_fwd_ring<G>), dim3((unsigned)nblk, (unsigned)nsplit),
+                        dim3(G::THREADS), G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1,
+                        (const float*)in2, (float*)out, C, H, W, Ho, Wo, off, layout, divisor,
+                        inv, n_ty, n_tx, cps, (float*)partial
 #ifdef PWC_RING_CENSUS
-                     , g_census
+                        , g_census
 #endif
-                     );
+                        );
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nsplit == 1) return e;
   return corr_reduce_splits_f32(partial, out, (size_t)B * G::D * G::D * Ho * Wo, nsplit,

@@ -29,6 +29,7 @@ _IP = ctypes.POINTER(ctypes.c_int)
 SYMBOLS = {
     "pwc_abi_version": (_I, []),
     "pwc_last_error": (ctypes.c_char_p, []),
+    "pwc_time_next_corr": (_I, [_P, _P]),
     "pwc_corr_output_shape": (_I, [_I] * 7 + [_IP] * 3),
     "pwc_corr_forward": (_I, [_P, _P, _P] + [_I] * 11 + [_P]),
     "pwc_corr_workspace_size": (_Z, [_I] * 9),
@@ -41,7 +42,7 @@ SYMBOLS = {
     "pwc_warp_forward": (_I, [_P, _P, _P] + [_I] * 5 + [_P]),
     "pwc_warp_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 5 + [_P]),
 }
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lock = threading.Lock()
 _lib = None
