@@ -19,6 +19,7 @@
 // Generic kernel: any (pad, k, md, s1, s2), one thread per output element; used for the
 // rarely-used configurations the tiled kernel does not instantiate.
 #include <cmath>
+#include <cstdlib>
 
 #include "pwc_common.cuh"
 
@@ -318,16 +319,47 @@ __global__ void corr_fwd_generic(const T* __restrict__ in1, const T* __restrict_
 
 // Split-channel reduction: out[i] = (sum_k partial[k][i]) / divisor, k ascending (fixed order,
 // deterministic).  inv_divisor != 0 when the divisor is a power of two (exact scale).
+// out[i] = (sum_k partial[k][i]) / divisor, k = 0..nsplit-1 in order (deterministic).  All of
+// a thread's nsplit loads are issued before the in-order sum (nsplit <= kMaxSplits), four
+// consecutive elements per thread when n % 4 == 0.
 template <typename T>
 __global__ __launch_bounds__(256) void corr_reduce_splits(const float* __restrict__ partial,
                                                           T* __restrict__ out, size_t n,
                                                           int nsplit, float divisor,
                                                           float inv_divisor) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+  const bool vec = (n % 4) == 0;
+  const size_t nv = vec ? n / 4 : n;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv;
        i += (size_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += partial[(size_t)k * n + i];
-    out[i] = from_f32<T>(inv_divisor != 0.f ? s * inv_divisor : s / divisor);
+    if (vec) {
+      float4 v[kMaxSplits];
+#pragma unroll
+      for (int k = 0; k < kMaxSplits; ++k)
+        if (k < nsplit) v[k] = reinterpret_cast<const float4*>(partial + (size_t)k * n)[i];
+      float4 s = v[0];
+#pragma unroll
+      for (int k = 1; k < kMaxSplits; ++k)
+        if (k < nsplit) {
+          s.x += v[k].x;
+          s.y += v[k].y;
+          s.z += v[k].z;
+          s.w += v[k].w;
+        }
+      const float r[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        out[4 * i + e] = from_f32<T>(inv_divisor != 0.f ? r[e] * inv_divisor : r[e] / divisor);
+    } else {
+      float v[kMaxSplits];
+#pragma unroll
+      for (int k = 0; k < kMaxSplits; ++k)
+        if (k < nsplit) v[k] = partial[(size_t)k * n + i];
+      float s = v[0];
+#pragma unroll
+      for (int k = 1; k < kMaxSplits; ++k)
+        if (k < nsplit) s += v[k];
+      out[i] = from_f32<T>(inv_divisor != 0.f ? s * inv_divisor : s / divisor);
+    }
   }
 }
 
@@ -341,7 +373,9 @@ template <typename T>
 static hipError_t corr_reduce_splits_t(const void* partial, void* out, size_t n, int nsplit,
                                        float divisor, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  size_t blocks = (n + 255) / 256;
+  if (nsplit < 1 || nsplit > kMaxSplits) return hipErrorInvalidValue;
+  const size_t nv = (n % 4 == 0) ? n / 4 : n;
+  size_t blocks = (nv + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(corr_reduce_splits<T>, dim3((unsigned)blocks), dim3(256), 0, stream,
                      (const float*)partial, (T*)out, n, nsplit, divisor,
@@ -423,6 +457,11 @@ hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, in
                                  int layout, float divisor, int max_splits, void* partial,
                                  hipStream_t stream);
 
+// corr_grp.hip
+hipError_t corr_forward_grp_f32(const void* in1, const void* in2, void* out, int B, int C, int H,
+                                int W, int Ho, int Wo, int off, int dr, int s2, int layout,
+                                float divisor, hipStream_t stream);
+
 // Channel-split budget: nsplit partial volumes of B*OC*Ho*Wo floats, nsplit <= kMaxSplits and
 // nsplit * volume <= kSplitBudget; no workspace once the 16x16 tiles alone fill the chip.
 constexpr size_t kSplitBudget = 16u << 20;
@@ -441,6 +480,16 @@ size_t corr_workspace_bytes(int B, int OC, int Ho, int Wo) {
   return k > 1 ? (size_t)k * B * OC * Ho * Wo * sizeof(float) : 0;
 }
 
+// PWC_CORR_GRP=0 disables the coarse-level kernel (measurement of the split path only).
+static bool grp_disabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = std::getenv("PWC_CORR_GRP");
+    v = (s && s[0] == '0') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 // `workspace` (>= corr_workspace_bytes) enables channel splitting for grids too small to fill
 // the chip; null keeps one workgroup per tile over all channels.
 template <typename T>
@@ -454,6 +503,15 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
   const int max_splits = workspace ? corr_max_splits(B, D * D, Ho, Wo) : 1;
   if (max_splits <= 1) workspace = nullptr;
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4) {
+    // coarse levels (too few 16x16 tiles to fill the chip) with 16-B aligned rows:
+    // in-workgroup channel groups (corr_grp.hip); unaligned rows (W % 4 != 0, the smallest
+    // pyramid levels) measured faster on the channel-split path below.
+    const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
+    if (tiles < 256 && W % 4 == 0 && (md - pad) % 4 == 0 && !grp_disabled()) {
+      const hipError_t e = corr_forward_grp_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad,
+                                                dr, s2, layout, divisor, stream);
+      if (e != hipErrorNotSupported) return e;
+    }
     const hipError_t e = corr_forward_ring_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad, dr,
                                                s2, layout, divisor, max_splits, workspace,
                                                stream);

@@ -141,27 +141,39 @@ struct RingTile {
 __constant__ int g_ablation;
 #endif
 
+// DMA of one stage.  The buffer resource is rebuilt per stage with its base at the stage's first
+// channel (scalar work only), so the per-lane voffsets stay the lane constants src_off and the
+// vector registers carry nothing stage-dependent; num_records shrinks with the base, so channels
+// past C still read zeros.  (The body is device-only: hipcc's host pass rejects the buffer
+// resource builtins in some template instantiation chains.)
 template <class G>
 __device__ __forceinline__ void ring_issue(int stage, int c_begin, int wave, uint32_t plane,
-                                           uint32_t lds0,
-                                           __amdgpu_buffer_rsrc_t rs1,
-                                           __amdgpu_buffer_rsrc_t rs2,
+                                           uint32_t lds0, const float* img1, const float* img2,
+                                           uint32_t img_bytes,
                                            const uint32_t (&src_off)[G::PPW],
                                            const uint32_t (&dst_off)[G::PPW],
                                            const bool (&from_f2)[G::PPW]) {
-  constexpr uint32_t kOOB = 0x80000000u;
+#if defined(__HIP_DEVICE_COMPILE__)
   if (wave >= G::ISSUERS) return;
-  const uint32_t cbytes = (uint32_t)(c_begin + stage * G::CC) * plane * 4u;  // channel advance
+  const uint32_t c0 = (uint32_t)(c_begin + stage * G::CC);
+  const uint32_t cbytes = c0 * plane * 4u;
+  const int nrec = cbytes < img_bytes ? (int)(img_bytes - cbytes) : 0;
   const uint32_t sbase = lds0 + (uint32_t)((stage % G::NS) * G::STAGE_FLOATS) * 4u;
 #pragma unroll
   for (int i = 0; i < G::PPW; ++i) {
-    // channels past C land at offsets >= num_records: zeros from the range check
-    const uint32_t vo = src_off[i] == kOOB ? kOOB : src_off[i] + cbytes;
+    // wave-uniform by construction; readfirstlane lets the compiler see it (else it wraps the
+    // DMA in a waterfall loop over "divergent" resource descriptors)
+    const uint64_t b = (uint64_t)(uintptr_t)(from_f2[i] ? img2 : img1) + (uint64_t)cbytes;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
+        __builtin_amdgcn_readfirstlane(nrec), 0x00020000);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        from_f2[i] ? rs2 : rs1,
-        (__attribute__((address_space(3))) void*)(uintptr_t)(sbase + dst_off[i]), 16, vo, 0, 0,
-        0);
+        rs, (__attribute__((address_space(3))) void*)(uintptr_t)(sbase + dst_off[i]), 16,
+        src_off[i], 0, 0, 0);
   }
+#endif
 }
 
 // Channel split (blockIdx.y = split k of nsplit): split k sums channels
@@ -196,10 +208,8 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
 
   const uint32_t plane = (uint32_t)(H * W);
   const uint32_t img_bytes = (uint32_t)C * plane * 4u;  // checked < 2^31 by the launcher
-  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(in1 + (size_t)n * C * plane), (short)0, (int)img_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(in2 + (size_t)n * C * plane), (short)0, (int)img_bytes, 0x00020000);
+  const float* img1 = in1 + (size_t)n * C * plane;
+  const float* img2 = in2 + (size_t)n * C * plane;
   const uint32_t lds0 = lds_addr(lds);
 
   // ---- DMA issue plan: issuer wave w owns pieces w*PPW .. w*PPW+PPW-1 of every stage ----
@@ -253,7 +263,8 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
 #pragma unroll
   for (int s = 0; s < G::NS - 1; ++s)
     if (s < nst)
-      ring_issue<G>(s, c_begin, wave, plane, lds0, rs1, rs2, src_off, dst_off, from_f2);
+      ring_issue<G>(s, c_begin, wave, plane, lds0, img1, img2, img_bytes, src_off, dst_off,
+                    from_f2);
 
   for (int st = 0; st < nst; ++st) {
 #if !(defined(PWC_RING_ABL_MODE) && PWC_RING_ABL_MODE == 3)  // 3: no DMA, no barriers
@@ -269,8 +280,8 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     if (g_ablation != 2)
 #endif
     if (st + G::NS - 1 < nst)
-      ring_issue<G>(st + G::NS - 1, c_begin, wave, plane, lds0, rs1, rs2, src_off, dst_off,
-                    from_f2);
+      ring_issue<G>(st + G::NS - 1, c_begin, wave, plane, lds0, img1, img2, img_bytes, src_off,
+                    dst_off, from_f2);
     const uint32_t sb = lds0 + (uint32_t)((st % G::NS) * G::STAGE_FLOATS) * 4u;
 #ifdef PWC_RING_ABLATION
     if (g_ablation == 1) continue;
@@ -285,10 +296,11 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    census[blockIdx.x * 4 + 0] = hw;
-    census[blockIdx.x * 4 + 1] = xcc;
-    census[blockIdx.x * 4 + 2] = (unsigned)census_t0;
-    census[blockIdx.x * 4 + 3] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    const unsigned cb = blockIdx.y * gridDim.x + blockIdx.x;
+    census[cb * 4 + 0] = hw;
+    census[cb * 4 + 1] = xcc;
+    census[cb * 4 + 2] = (unsigned)census_t0;
+    census[cb * 4 + 3] = (unsigned)__builtin_amdgcn_s_memrealtime();
   }
 #endif
   // ---- epilogue: out = acc / divisor (cu:100); a power-of-two divisor is an exact scale ----
@@ -321,6 +333,283 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
       v = make_float4(acc[ti][0] / divisor, acc[ti][1] / divisor, acc[ti][2] / divisor,
                       acc[ti][3] / divisor);
     *reinterpret_cast<float4*>(orow + ox) = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Software-pipelined ring kernel (same tile, waves, DMA ring and LDS image as corr_fwd_ring).
+// The per-channel "6 reads, wait for all, 36 FMAs" of corr_fwd_ring leaves every wave idle for
+// an LDS round trip per channel, and at <= 4.5 waves per SIMD the other waves do not cover it
+// (measured: VALU and the LDS array each < 25 % busy).  Here a lane's reads for channel c+1
+// are issued into the registers channel c has finished with, in the order channel c+1 needs
+// them, and each displacement ti waits only for its own quads (counted lgkmcnt):
+//   f1 quad A and window quads Q0..Q4 of channel c+1 go out after ti = 1, 3, 5, 7, 8 of
+//   channel c, so 4 reads stay in flight under the FMAs (A is double-buffered: 4 VGPRs).
+// The stage barrier moves into the last channel of a stage (after ti = 1, before the first
+// read of the next stage), so the ring keeps NS-2 stages in flight instead of NS-1.  Stages
+// are unrolled NS at a time so every LDS offset (slot, channel) is an instruction immediate.
+// ------------------------------------------------------------------------------------
+template <int OFF>
+__device__ __forceinline__ f32x4 lds_rd(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  f32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF) : "memory");
+  return r;
+}
+
+// Wait until at most N LDS operations are outstanding.  The registers the wait completes are
+// tied through it, so the compiler neither reads them earlier nor reuses them meanwhile (it
+// does not know the reads above were asynchronous).
+template <int N>
+__device__ __forceinline__ void lgk_wait(f32x4& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void lgk_wait(f32x4& a, f32x4& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
+}
+
+template <class G>
+struct PipeState {
+  float acc[G::D][G::PX];
+  f32x4 A[2];      // f1 quad, double-buffered by channel parity
+  f32x4 Q[5];      // f2 window quads
+  uint32_t aA;     // lane LDS byte addresses (channel 0 of slot 0); slot/channel = immediate
+  uint32_t aW[5];
+};
+
+// The FMAs of one displacement; the scheduling barrier keeps them between the waits and
+// read issues around them (left alone, the scheduler sinks them past the next reads and the
+// stage barrier, lengthening register live ranges until the kernel spills).
+template <class G, int TI>
+__device__ __forceinline__ void pipe_fma(PipeState<G>& s, const f32x4& a) {
+#pragma unroll
+  for (int k = 0; k < G::PX; ++k) {
+    const int j = k + G::S * TI;
+    s.acc[TI][k] = fmaf(a[k], s.Q[j >> 2][j & 3], s.acc[TI][k]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Issue reads of the channel stored at immediate offset OFF into A[P] / Q[u].
+template <class G, int OFF, int P>
+__device__ __forceinline__ void pipe_issue_a_q0(PipeState<G>& s) {
+  s.A[P] = lds_rd<OFF>(s.aA);
+  s.Q[0] = lds_rd<OFF>(s.aW[0]);
+}
+
+struct PipeRing {  // per-block constants of the DMA ring
+  const float* img1;
+  const float* img2;
+  uint32_t plane, lds0, img_bytes;
+  int c_begin, wave, nst;
+};
+
+// One channel: slot RS of the unrolled round, channel CI of the stage, runtime stage st.
+template <class G, int RS, int CI>
+__device__ __forceinline__ void pipe_channel(PipeState<G>& s, PipeRing& r, int st,
+                                             const uint32_t (&src_off)[G::PPW],
+                                             const uint32_t (&dst_off)[G::PPW],
+                                             const bool (&from_f2)[G::PPW]) {
+  constexpr int SLOT_B = G::STAGE_FLOATS * 4, CH_B = G::CH_FLOATS * 4;
+  constexpr bool LAST = CI == G::CC - 1;
+  constexpr int NRS = LAST ? (RS + 1) % G::NS : RS;  // next channel's slot and channel
+  constexpr int NCI = LAST ? 0 : CI + 1;
+  constexpr int NOFF = NRS * SLOT_B + NCI * CH_B;
+  constexpr int P = (RS * G::CC + CI) & 1;
+  static_assert((G::NS * G::CC) % 2 == 0, "f1 parity must repeat every round");
+
+  lgk_wait<4>(s.A[P], s.Q[0]);
+  pipe_fma<G, 0>(s, s.A[P]);
+  lgk_wait<3>(s.Q[1]);
+  pipe_fma<G, 1>(s, s.A[P]);
+  if constexpr (LAST) {
+    // stage barrier: stage st+1 must have landed (issuers' counted vmcnt), and every wave is
+    // past all reads of stage st-1, whose slot the DMA for stage st+NS-1 now refills.
+    if (st + 1 < r.nst) {
+      if (r.wave < G::ISSUERS) {
+        if (r.nst - 2 - st >= G::NS - 3)
+          wait_vmcnt<(G::NS - 3) * G::PPW>();
+        else
+          wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      if (st + G::NS - 1 < r.nst)
+        ring_issue<G>(st + G::NS - 1, r.c_begin, r.wave, r.plane, r.lds0, r.img1, r.img2,
+                      r.img_bytes, src_off, dst_off, from_f2);
+    }
+  }
+  // (after the last stage these reads re-read live LDS and are discarded)
+  pipe_issue_a_q0<G, NOFF, P ^ 1>(s);
+  pipe_fma<G, 2>(s, s.A[P]);
+  lgk_wait<4>(s.Q[2]);
+  pipe_fma<G, 3>(s, s.A[P]);
+  s.Q[1] = lds_rd<NOFF>(s.aW[1]);
+  pipe_fma<G, 4>(s, s.A[P]);
+  lgk_wait<4>(s.Q[3]);
+  pipe_fma<G, 5>(s, s.A[P]);
+  s.Q[2] = lds_rd<NOFF>(s.aW[2]);
+  pipe_fma<G, 6>(s, s.A[P]);
+  lgk_wait<4>(s.Q[4]);
+  pipe_fma<G, 7>(s, s.A[P]);
+  s.Q[3] = lds_rd<NOFF>(s.aW[3]);
+  pipe_fma<G, 8>(s, s.A[P]);
+  s.Q[4] = lds_rd<NOFF>(s.aW[4]);
+}
+
+template <class G, int RS, int CI>
+__device__ __forceinline__ void pipe_stage(PipeState<G>& s, PipeRing& r, int st,
+                                           const uint32_t (&src_off)[G::PPW],
+                                           const uint32_t (&dst_off)[G::PPW],
+                                           const bool (&from_f2)[G::PPW]) {
+  if constexpr (CI < G::CC) {
+    pipe_channel<G, RS, CI>(s, r, st, src_off, dst_off, from_f2);
+    pipe_stage<G, RS, CI + 1>(s, r, st, src_off, dst_off, from_f2);
+  }
+}
+
+// Stages st0+RS .. st0+NS-1 of one unrolled round; false once the block's stages are done.
+template <class G, int RS>
+__device__ __forceinline__ bool pipe_round(PipeState<G>& s, PipeRing& r, int st0,
+                                           const uint32_t (&src_off)[G::PPW],
+                                           const uint32_t (&dst_off)[G::PPW],
+                                           const bool (&from_f2)[G::PPW]) {
+  if constexpr (RS < G::NS) {
+    if (st0 + RS >= r.nst) return false;
+    pipe_stage<G, RS, 0>(s, r, st0 + RS, src_off, dst_off, from_f2);
+    return pipe_round<G, RS + 1>(s, r, st0, src_off, dst_off, from_f2);
+  }
+  return true;
+}
+
+template <class G>
+__global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ringp(
+    const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
+    int C, int H, int W, int Ho, int Wo, int off, int layout, float divisor, float inv_divisor,
+    int n_ty, int n_tx, int cps, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  static_assert(G::NS >= 3, "pipelined ring keeps NS-2 stages in flight");
+  static_assert((G::NS - 1) * G::STAGE_FLOATS * 4 + (G::CC - 1) * G::CH_FLOATS * 4 < 65536,
+                "slot/channel offsets must fit the ds offset field");
+
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tx_tile = t % n_tx;
+  const int ty_tile = (t / n_tx) % n_ty;
+  const int n = t / (n_tx * n_ty);
+  const int oy0 = ty_tile * G::TY, ox0 = tx_tile * G::TX;
+  const int y1 = oy0 + off, x1 = ox0 + off;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = threadIdx.x % G::NQ;
+  const int ty = (threadIdx.x / G::NQ) % G::TY;
+  const int tjx = threadIdx.x / (G::NQ * G::TY);
+
+  PipeRing r;
+  r.plane = (uint32_t)(H * W);
+  const uint32_t img_bytes = (uint32_t)C * r.plane * 4u;
+  r.img1 = in1 + (size_t)n * C * r.plane;
+  r.img2 = in2 + (size_t)n * C * r.plane;
+  r.img_bytes = img_bytes;
+  r.lds0 = lds_addr(lds);
+  r.wave = wave;
+
+  uint32_t src_off[G::PPW];
+  uint32_t dst_off[G::PPW];
+  bool from_f2[G::PPW];
+  constexpr uint32_t kOOB = 0x80000000u;
+  if (wave < G::ISSUERS) {
+#pragma unroll
+    for (int i = 0; i < G::PPW; ++i) {
+      const int p = wave * G::PPW + i;
+      const int cc = p / (G::F2P + G::F1P);
+      const int k = p % (G::F2P + G::F1P);
+      int gy, gx;
+      uint32_t dst = (uint32_t)(cc * G::CH_FLOATS) * 4u;
+      if (k < G::F2P) {
+        const int rr = 8 * k + (lane >> 3);
+        const int srcq = (lane & 7) ^ (((rr >> 1) & 1) << 2);
+        gy = y1 - G::HALO + rr;
+        gx = x1 - G::HALO + 4 * srcq;
+        dst += (uint32_t)(8 * k * G::X2) * 4u;
+      } else {
+        gy = y1 + (lane >> 2);
+        gx = x1 + 4 * (lane & 3);
+        dst += (uint32_t)G::F2_FLOATS * 4u;
+      }
+      const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+      src_off[i] = ok ? ((uint32_t)cc * r.plane + (uint32_t)(gy * W + gx)) * 4u : kOOB;
+      dst_off[i] = dst;
+      from_f2[i] = k < G::F2P;
+    }
+  }
+
+  PipeState<G> s;
+  const int r2 = ty + G::S * tjx;
+  const int sw = ((r2 >> 1) & 1) << 2;
+#pragma unroll
+  for (int u = 0; u < 5; ++u)
+    s.aW[u] = r.lds0 + (uint32_t)(r2 * G::X2 + (((q + u) ^ sw) << 2)) * 4u;
+  s.aA = r.lds0 + (uint32_t)(G::F2_FLOATS + ty * G::TX + (q << 2)) * 4u;
+#pragma unroll
+  for (int a = 0; a < G::D; ++a)
+#pragma unroll
+    for (int k = 0; k < G::PX; ++k) s.acc[a][k] = 0.f;
+
+  r.c_begin = blockIdx.y * cps;
+  const int c_end = min(C, r.c_begin + cps);
+  r.nst = (c_end - r.c_begin + G::CC - 1) / G::CC;
+  if (r.nst > 0) {
+#pragma unroll
+    for (int st = 0; st < G::NS - 1; ++st)
+      if (st < r.nst)
+        ring_issue<G>(st, r.c_begin, wave, r.plane, r.lds0, r.img1, r.img2, r.img_bytes, src_off,
+                      dst_off, from_f2);
+    if (wave < G::ISSUERS) {
+      if (r.nst - 1 >= G::NS - 2)
+        wait_vmcnt<(G::NS - 2) * G::PPW>();
+      else
+        wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    pipe_issue_a_q0<G, 0, 0>(s);
+#pragma unroll
+    for (int u = 1; u < 5; ++u) s.Q[u] = lds_rd<0>(s.aW[u]);
+    for (int st0 = 0;; st0 += G::NS)
+      if (!pipe_round<G, 0>(s, r, st0, src_off, dst_off, from_f2)) break;
+    // drain the discarded reads before their registers can be reused
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(s.A[0]), "+v"(s.A[1]), "+v"(s.Q[0]), "+v"(s.Q[1]), "+v"(s.Q[2]),
+                   "+v"(s.Q[3]), "+v"(s.Q[4]));
+  }
+
+  const int oy = oy0 + ty;
+  const int ox = ox0 + 4 * q;
+  if (oy >= Ho || ox >= Wo) return;
+  const int OC = G::D * G::D;
+  const int tj = tjx - G::DR;
+  if (gridDim.y > 1) {
+    float* pk = partial + (size_t)blockIdx.y * ((size_t)gridDim.x / (n_tx * n_ty)) * OC * Ho * Wo;
+#pragma unroll
+    for (int ti = 0; ti < G::D; ++ti) {
+      const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
+      *reinterpret_cast<float4*>(pk + (((size_t)n * OC + oc) * Ho + oy) * Wo + ox) =
+          make_float4(s.acc[ti][0], s.acc[ti][1], s.acc[ti][2], s.acc[ti][3]);
+    }
+    return;
+  }
+  const bool pow2 = inv_divisor != 0.f;
+#pragma unroll
+  for (int ti = 0; ti < G::D; ++ti) {
+    const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
+    float4 v;
+    if (pow2)
+      v = make_float4(s.acc[ti][0] * inv_divisor, s.acc[ti][1] * inv_divisor,
+                      s.acc[ti][2] * inv_divisor, s.acc[ti][3] * inv_divisor);
+    else
+      v = make_float4(s.acc[ti][0] / divisor, s.acc[ti][1] / divisor, s.acc[ti][2] / divisor,
+                      s.acc[ti][3] / divisor);
+    *reinterpret_cast<float4*>(out + (((size_t)n * OC + oc) * Ho + oy) * Wo + ox) = v;
   }
 }
 
@@ -653,12 +942,54 @@ static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B
                                 divisor, inv, stream);
 }
 
+template <class G>
+static hipError_t launch_ringp(const void* in1, const void* in2, void* out, int B, int C, int H,
+                               int W, int Ho, int Wo, int off, int layout, float divisor,
+                               int nsplit, void* partial, hipStream_t stream) {
+  const int n_ty = (Ho + G::TY - 1) / G::TY;
+  const int n_tx = (Wo + G::TX - 1) / G::TX;
+  const long long nblk = (long long)B * n_ty * n_tx;
+  if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_ringp<G>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int nchunks = (C + G::CC - 1) / G::CC;
+  if (nsplit > nchunks) nsplit = nchunks;
+  if (nsplit < 1) nsplit = 1;
+  const int cps = ((nchunks + nsplit - 1) / nsplit) * G::CC;
+  nsplit = (C + cps - 1) / cps;
+  int ex;
+  const float m = std::frexp(divisor, &ex);
+  const float inv = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  take_launch_events(&ev0, &ev1);
+  hipExtLaunchKernelGGL((corr_fwd_ringp<G>), dim3((unsigned)nblk, (unsigned)nsplit),
+                        dim3(G::THREADS), G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1,
+                        (const float*)in2, (float*)out, C, H, W, Ho, Wo, off, layout, divisor,
+                        inv, n_ty, n_tx, cps, (float*)partial);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nsplit == 1) return e;
+  return corr_reduce_splits_f32(partial, out, (size_t)B * G::D * G::D * Ho * Wo, nsplit,
+                                divisor, inv, stream);
+}
+
+using RingPJ = RingTile<4, 2, 16, 2, 6, 2>;   // 60 KiB, 4 stages (8 channels) in flight
+using RingPK = RingTile<4, 2, 16, 1, 12, 1>;  // 60 KiB, 10 single-channel stages in flight
+using RingPL = RingTile<4, 2, 16, 3, 4, 3>;   // 60 KiB, 2 stages (6 channels) in flight
+using RingPM = RingTile<4, 2, 16, 2, 5, 2>;   // 50 KiB, 3 stages (6 channels) in flight
+
 static int ring_cfg() {
   static int v = -1;
   if (v < 0) {
     const char* s = std::getenv("PWC_RING_CFG");
     v = 2;  // default: C
-    if (s && s[0] >= 'A' && s[0] <= 'I' && s[1] == 0) v = s[0] - 'A';
+    if (s && s[0] >= 'A' && s[0] <= 'M' && s[1] == 0) v = s[0] - 'A';
   }
   return v;
 }
@@ -697,6 +1028,10 @@ hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, in
     case 6: return launch_ringdi<RingDiG>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
     case 7: return launch_ringdi<RingDiH>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
     case 8: return launch_ringdi<RingDiI>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 9: return launch_ringp<RingPJ>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 10: return launch_ringp<RingPK>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 11: return launch_ringp<RingPL>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 12: return launch_ringp<RingPM>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
     default: return launch_ring<RingC>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
   }
 }

@@ -83,6 +83,46 @@ __device__ __forceinline__ Corners corners(const Bilinear& b, int H, int W) {
 
 __device__ __forceinline__ float masked(float v, float m) { return m != 0.f ? v : 0.f; }
 
+// Horizontal corner pairs: both corners of a sample row come from ONE 8-byte load at
+// xs = clamp(x0, 0, W-2) (dword-aligned, which global loads accept), halving the gather
+// instructions -- the texture-address unit, not HBM, bounds this kernel.  Corner x0 is
+// element x0 - xs of the pair, corner x0+1 element x0 + 1 - xs; out-of-image corners are
+// masked as before.  (W == 1 keeps single loads.)
+typedef float f32x2u __attribute__((ext_vector_type(2), aligned(4)));
+
+struct Pairs {
+  unsigned i0, i1;       // row starts of the two sample rows + xs (element index in the plane)
+  bool l_lo, r_lo;       // left / right corner is the pair's low element
+  float m00, m01, m10, m11;
+};
+
+__device__ __forceinline__ Pairs pairs(const Bilinear& b, int H, int W) {
+  Pairs p;
+  const int xs = min(max(b.x0, 0), W - 2);
+  const int y0 = min(max(b.y0, 0), H - 1), y1 = min(max(b.y0 + 1, 0), H - 1);
+  p.i0 = (unsigned)(y0 * W + xs);
+  p.i1 = (unsigned)(y1 * W + xs);
+  p.l_lo = b.x0 == xs;
+  p.r_lo = b.x0 + 1 == xs;
+  p.m00 = (b.vy0 && b.vx0) ? 1.f : 0.f;
+  p.m01 = (b.vy0 && b.vx1) ? 1.f : 0.f;
+  p.m10 = (b.vy1 && b.vx0) ? 1.f : 0.f;
+  p.m11 = (b.vy1 && b.vx1) ? 1.f : 0.f;
+  return p;
+}
+
+template <typename T>
+__device__ __forceinline__ void load_pair(const T* p, float& lo, float& hi) {
+  if constexpr (sizeof(T) == 4) {
+    const f32x2u v = *reinterpret_cast<const f32x2u*>(p);
+    lo = v.x;
+    hi = v.y;
+  } else {
+    lo = to_f32(p[0]);
+    hi = to_f32(p[1]);
+  }
+}
+
 // One thread per output pixel and CB channels (grid.y splits the channels).  32-bit indexing
 // (the launcher checks B*C*H*W < 2^31).
 template <typename T, int CB>
@@ -102,27 +142,49 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
   const float ix = src_coord(u, px, W, halfx);
   const float iy = src_coord(v, py, H, halfy);
   const Bilinear b = bilinear(ix, iy, H, W);
-  const Corners k = corners(b, H, W);
   const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;  // feed fma operands: not fusable
   const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
   const int c0 = blockIdx.y * CB;
   float r[CB][4];
+  float m00, m01, m10, m11;
+  if (W >= 2) {
+    const Pairs k = pairs(b, H, W);
+    m00 = k.m00; m01 = k.m01; m10 = k.m10; m11 = k.m11;
+    float lo[CB][2], hi[CB][2];
 #pragma unroll
-  for (int i = 0; i < CB; ++i) {
-    const int c = min(c0 + i, C - 1);
-    const T* p = x + ((unsigned)(n * C + c)) * plane;
-    r[i][0] = to_f32(p[k.i00]);
-    r[i][1] = to_f32(p[k.i01]);
-    r[i][2] = to_f32(p[k.i10]);
-    r[i][3] = to_f32(p[k.i11]);
+    for (int i = 0; i < CB; ++i) {
+      const int c = min(c0 + i, C - 1);
+      const T* p = x + ((unsigned)(n * C + c)) * plane;
+      load_pair(p + k.i0, lo[i][0], hi[i][0]);
+      load_pair(p + k.i1, lo[i][1], hi[i][1]);
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      r[i][0] = k.l_lo ? lo[i][0] : hi[i][0];
+      r[i][1] = k.r_lo ? lo[i][0] : hi[i][0];
+      r[i][2] = k.l_lo ? lo[i][1] : hi[i][1];
+      r[i][3] = k.r_lo ? lo[i][1] : hi[i][1];
+    }
+  } else {
+    const Corners k = corners(b, H, W);
+    m00 = k.m00; m01 = k.m01; m10 = k.m10; m11 = k.m11;
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = min(c0 + i, C - 1);
+      const T* p = x + ((unsigned)(n * C + c)) * plane;
+      r[i][0] = to_f32(p[k.i00]);
+      r[i][1] = to_f32(p[k.i01]);
+      r[i][2] = to_f32(p[k.i10]);
+      r[i][3] = to_f32(p[k.i11]);
+    }
   }
 #pragma unroll
   for (int i = 0; i < CB; ++i) {
     float acc = 0.f;
-    acc = fmaf(masked(r[i][0], k.m00), w00, acc);
-    acc = fmaf(masked(r[i][1], k.m01), w01, acc);
-    acc = fmaf(masked(r[i][2], k.m10), w10, acc);
-    acc = fmaf(masked(r[i][3], k.m11), w11, acc);
+    acc = fmaf(masked(r[i][0], m00), w00, acc);
+    acc = fmaf(masked(r[i][1], m01), w01, acc);
+    acc = fmaf(masked(r[i][2], m10), w10, acc);
+    acc = fmaf(masked(r[i][3], m11), w11, acc);
     if (c0 + i < C) out[((unsigned)(n * C + c0 + i)) * plane + pix] = from_f32<T>(acc);
   }
 }

@@ -17,7 +17,9 @@ import threading
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libpwc_hotpath.so")
+# PWC_HOTPATH_LIB overrides the library path (diagnostic builds, e.g. tools/ ablations).
+LIB_PATH = os.environ.get("PWC_HOTPATH_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "lib", "libpwc_hotpath.so")
 
 DTYPE_CODES = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
 

@@ -29,7 +29,9 @@ int main(int argc, char** argv) {
   report<RingA>("RingA");
   report<RingB>("RingB");
   report<RingC>("RingC");
-  const int B = argc > 1 ? atoi(argv[1]) : 7, C = 32, H = 96, W = 112;
+  const int B = argc > 1 ? atoi(argv[1]) : 7;
+  const int C = argc > 3 ? atoi(argv[3]) : 32, H = argc > 4 ? atoi(argv[4]) : 96,
+            W = argc > 5 ? atoi(argv[5]) : 112, maxs = argc > 6 ? atoi(argv[6]) : 1;
 #ifdef PWC_RING_ABLATION
   {
     const int abl = argc > 2 ? atoi(argv[2]) : 0;
@@ -44,10 +46,15 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&o, (size_t)B * 81 * H * W * 4);
   (void)hipMemset(a, 0, n * 4);
   (void)hipMemset(b, 0, n * 4);
-  const int nb = B * 6 * 7;
+  const long long tiles = (long long)B * ((H + 15) / 16) * ((W + 15) / 16);
+  const int ns = corr_pick_splits(tiles, (C + 3) / 4, maxs);
+  const int nb = (int)tiles * ns;
+  printf("B=%d C=%d %dx%d: %lld tiles x %d splits\n", B, C, H, W, tiles, ns);
+  float* part = nullptr;
+  if (maxs > 1) (void)hipMalloc(&part, (size_t)maxs * B * 81 * H * W * 4);
   (void)hipMalloc(&g_census, nb * 16);
   for (int rep = 0; rep < 3; ++rep)
-    (void)corr_forward_ring_f32(a, b, o, B, C, H, W, H, W, 0, 4, 2, 0, 32.f, 1, nullptr, 0);
+    (void)corr_forward_ring_f32(a, b, o, B, C, H, W, H, W, 0, 4, 2, 0, 32.f, maxs, part, 0);
   (void)hipDeviceSynchronize();
   {
     hipEvent_t e0, e1;
@@ -55,7 +62,7 @@ int main(int argc, char** argv) {
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, 0);
     for (int rep = 0; rep < 50; ++rep)
-      (void)corr_forward_ring_f32(a, b, o, B, C, H, W, H, W, 0, 4, 2, 0, 32.f, 1, nullptr, 0);
+      (void)corr_forward_ring_f32(a, b, o, B, C, H, W, H, W, 0, 4, 2, 0, 32.f, maxs, part, 0);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0;
