@@ -261,7 +261,7 @@ def main():
             "graph": bool(graphs),
         },
         "roofline": {
-            "kernel": "corr_fwd_ring<RingC> at l4 (32x96x112, B=8)",
+            "kernel": "corr_fwd_ring<RingN> at l4 (32x96x112, B=8)",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,

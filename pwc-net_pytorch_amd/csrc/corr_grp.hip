@@ -132,13 +132,8 @@ __device__ __forceinline__ void grp_stage(uint32_t a0, uint32_t a1, uint32_t a2,
   if constexpr (I < G::CC) {
     f32x4 fa, b0, b1, b2, b3, b4;
     lds_read6<I * G::CH_FLOATS * 4>(a0, a1, a2, a3, a4, a5, fa, b0, b1, b2, b3, b4);
-    const float av[4] = {fa.x, fa.y, fa.z, fa.w};
-    const float w[20] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y,
-                         b2.z, b2.w, b3.x, b3.y, b3.z, b3.w, b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-    for (int ti = 0; ti < G::D; ++ti)
-#pragma unroll
-      for (int k = 0; k < G::PX; ++k) acc[ti][k] = fmaf(av[k], w[k + G::S * ti], acc[ti][k]);
+    const f32x4 b[5] = {b0, b1, b2, b3, b4};
+    corr_fma_pairs_s2<G::D, 5>(acc, fa, b);
     grp_stage<G, I + 1>(a0, a1, a2, a3, a4, a5, acc);
   }
 }

@@ -85,19 +85,8 @@ __device__ __forceinline__ void ring_channel(const uint32_t (&addr)[6], float (&
   asm volatile("" ::"v"(a4), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]));
   return;
 #endif
-  const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-  float w[4 * G::NWQ];
-#pragma unroll
-  for (int u = 0; u < G::NWQ; ++u) {
-    w[4 * u + 0] = b[u].x;
-    w[4 * u + 1] = b[u].y;
-    w[4 * u + 2] = b[u].z;
-    w[4 * u + 3] = b[u].w;
-  }
-#pragma unroll
-  for (int ti = 0; ti < G::D; ++ti)
-#pragma unroll
-    for (int k = 0; k < G::PX; ++k) acc[ti][k] = fmaf(av[k], w[k + G::S * ti], acc[ti][k]);
+  static_assert(G::S == 2 && G::PX == 4, "packed pixel pairs need stride-2 displacements");
+  corr_fma_pairs_s2<G::D, G::NWQ>(acc, a4, b);
 }
 
 template <class G, int CC_I>
@@ -108,16 +97,20 @@ __device__ __forceinline__ void ring_stage(const uint32_t (&addr)[6], float (&ac
   }
 }
 
-template <int DR_, int S_, int TY_, int CC_, int NS_, int PPW_>
+// JG: displacement rows tj per workgroup (one wave each); a tile's D rows are spread over
+// D / JG workgroups, each staging only the f2 rows its tj need (TY + S*(JG-1), padded to whole
+// 8-row DMA pieces): more, smaller workgroups for grids with few tiles per CU.
+template <int DR_, int S_, int TY_, int CC_, int NS_, int PPW_, int JG_ = 2 * DR_ + 1>
 struct RingTile {
-  static constexpr int DR = DR_, S = S_, TY = TY_, CC = CC_, NS = NS_, PPW = PPW_;
+  static constexpr int DR = DR_, S = S_, TY = TY_, CC = CC_, NS = NS_, PPW = PPW_, JG = JG_;
   static constexpr int D = 2 * DR + 1;
+  static constexpr int NTJG = D / JG;
   static constexpr int HALO = DR * S;
   static constexpr int TX = 16, NQ = 4, PX = 4;
   static constexpr int X2 = 32;  // f2 tile row: 8 quads
-  static constexpr int R2 = TY + 2 * HALO;
+  static constexpr int R2 = ((TY + S * (JG - 1) + 7) / 8) * 8;
   static constexpr int NWQ = (PX + 2 * DR * S) / 4;  // f2 window quads per lane
-  static constexpr int THREADS = TY * NQ * D;
+  static constexpr int THREADS = TY * NQ * JG;
   static constexpr int F2_FLOATS = R2 * X2;
   static constexpr int F1_FLOATS = TY * TX;
   static constexpr int CH_FLOATS = F2_FLOATS + F1_FLOATS;
@@ -135,6 +128,7 @@ struct RingTile {
   static_assert((NWQ - 1) + (NQ - 1) < 8, "window inside the row");
   static_assert(THREADS % 64 == 0 && THREADS <= 1024, "workgroup");
   static_assert(NS >= 2, "ring depth");
+  static_assert(D % JG == 0, "tj groups");
 };
 
 #ifdef PWC_RING_ABLATION
@@ -191,14 +185,20 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #ifdef PWC_RING_CENSUS  // diagnostic build only (tools/occupancy.hip): residency census
   unsigned long long census_t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long census_c0 = __builtin_amdgcn_s_memtime();
+  unsigned long long census_c1 = 0, census_r1 = 0;
 #endif
 
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int tjg = t0 % G::NTJG;  // the tj groups of a tile are neighbours: same XCD
+  const int t = t0 / G::NTJG;
   const int tx_tile = t % n_tx;
   const int ty_tile = (t / n_tx) % n_ty;
   const int n = t / (n_tx * n_ty);
   const int oy0 = ty_tile * G::TY, ox0 = tx_tile * G::TX;
   const int y1 = oy0 + off, x1 = ox0 + off;  // f1 tile origin, unpadded image coordinates
+  const int tj0 = tjg * G::JG;
+  const int f2y0 = y1 - G::HALO + G::S * tj0;  // image row of f2 tile row 0
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
       if (k < G::F2P) {
         const int r = 8 * k + (lane >> 3);
         const int srcq = (lane & 7) ^ (((r >> 1) & 1) << 2);
-        gy = y1 - G::HALO + r;
+        gy = f2y0 + r;
         gx = x1 - G::HALO + 4 * srcq;
         dst += (uint32_t)(8 * k * G::X2) * 4u;
       } else {
@@ -266,6 +266,10 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
       ring_issue<G>(s, c_begin, wave, plane, lds0, img1, img2, img_bytes, src_off, dst_off,
                     from_f2);
 
+#ifdef PWC_RING_CENSUS
+  census_c1 = __builtin_amdgcn_s_memtime();
+  census_r1 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int st = 0; st < nst; ++st) {
 #if !(defined(PWC_RING_ABL_MODE) && PWC_RING_ABL_MODE == 3)  // 3: no DMA, no barriers
     if (wave < G::ISSUERS) {
@@ -297,10 +301,15 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     const unsigned cb = blockIdx.y * gridDim.x + blockIdx.x;
-    census[cb * 4 + 0] = hw;
-    census[cb * 4 + 1] = xcc;
-    census[cb * 4 + 2] = (unsigned)census_t0;
-    census[cb * 4 + 3] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    const unsigned long long c2 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r2 = __builtin_amdgcn_s_memrealtime();
+    census[cb * 8 + 0] = hw;
+    census[cb * 8 + 1] = xcc;
+    census[cb * 8 + 2] = (unsigned)census_t0;
+    census[cb * 8 + 3] = (unsigned)r2;
+    census[cb * 8 + 4] = (unsigned)(census_c1 - census_c0);  // prologue, shader cycles
+    census[cb * 8 + 5] = (unsigned)(c2 - census_c1);         // stage loop, shader cycles
+    census[cb * 8 + 6] = (unsigned)(r2 - census_r1);         // stage loop, 100 MHz ticks
   }
 #endif
   // ---- epilogue: out = acc / divisor (cu:100); a power-of-two divisor is an exact scale ----
@@ -308,9 +317,10 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
   const int ox = ox0 + 4 * q;
   if (oy >= Ho || ox >= Wo) return;
   const int OC = G::D * G::D;
-  const int tj = tjx - G::DR;
+  const int tj = tj0 + tjx - G::DR;
   if (gridDim.y > 1) {  // split: raw partial sums, reduced by corr_reduce_splits
-    float* pk = partial + (size_t)blockIdx.y * ((size_t)gridDim.x / (n_tx * n_ty)) * OC * Ho * Wo;
+    float* pk = partial + (size_t)blockIdx.y * ((size_t)gridDim.x / (n_tx * n_ty * G::NTJG)) *
+                              OC * Ho * Wo;
 #pragma unroll
     for (int ti = 0; ti < G::D; ++ti) {
       const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
@@ -893,6 +903,12 @@ using RingB = RingTile<4, 2, 16, 4, 4, 4>;  // 80 KiB, 3 in flight
 using RingC = RingTile<4, 2, 16, 2, 6, 2>;  // 60 KiB, 5 in flight
 using RingD = RingTile<4, 2, 16, 3, 5, 3>;  // 75 KiB, 4 in flight
 using RingE = RingTile<4, 2, 16, 2, 8, 2>;  // 80 KiB, 7 in flight
+// three workgroups per tile (3 tj rows each, 24-row f2 tiles): 3x the workgroups of RingC
+using RingN = RingTile<4, 2, 16, 2, 5, 4, 3>;  // 40 KiB, 4 stages in flight
+using RingO = RingTile<4, 2, 16, 3, 3, 4, 3>;  // 36 KiB, 2 in flight
+using RingP = RingTile<4, 2, 16, 2, 4, 4, 3>;  // 32 KiB, 3 in flight
+using RingQ = RingTile<4, 2, 16, 2, 8, 4, 3>;  // 64 KiB: 2 workgroups/CU, later ones staggered
+using RingR = RingTile<4, 2, 16, 2, 14, 4, 3>; // 112 KiB: 1 workgroup/CU
 
 #ifdef PWC_RING_CENSUS
 unsigned* g_census = nullptr;
@@ -904,7 +920,7 @@ static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B
                               int nsplit, void* partial, hipStream_t stream) {
   const int n_ty = (Ho + G::TY - 1) / G::TY;
   const int n_tx = (Wo + G::TX - 1) / G::TX;
-  const long long nblk = (long long)B * n_ty * n_tx;
+  const long long nblk = (long long)B * n_ty * n_tx * G::NTJG;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   static bool attr_set = false;
@@ -988,8 +1004,8 @@ static int ring_cfg() {
   static int v = -1;
   if (v < 0) {
     const char* s = std::getenv("PWC_RING_CFG");
-    v = 2;  // default: C
-    if (s && s[0] >= 'A' && s[0] <= 'M' && s[1] == 0) v = s[0] - 'A';
+    v = 13;  // default: N (3 workgroups per tile; measured 18.3 vs 19.9 us for C at l4, B 8)
+    if (s && s[0] >= 'A' && s[0] <= 'R' && s[1] == 0) v = s[0] - 'A';
   }
   return v;
 }
@@ -1032,7 +1048,12 @@ hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, in
     case 10: return launch_ringp<RingPK>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
     case 11: return launch_ringp<RingPL>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
     case 12: return launch_ringp<RingPM>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    default: return launch_ring<RingC>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 14: return launch_ring<RingO>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 15: return launch_ring<RingP>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 16: return launch_ring<RingQ>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 17: return launch_ring<RingR>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    case 2: return launch_ring<RingC>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
+    default: return launch_ring<RingN>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
   }
 }
 

@@ -10,6 +10,8 @@
 // (no FMA contraction), so sample coordinates match the reference chain.
 // Backward follows ATen grid_sampler_2d_backward: grad_x by fp32 atomics (scatter), grad of
 // the sample point by the bilinear derivative; d(ix)/d(u) = ((W-1)/2) / ((W-1)/2) = 1.
+#include <cstdlib>
+
 #include "pwc_common.cuh"
 
 namespace pwc {
@@ -126,12 +128,56 @@ __device__ __forceinline__ void load_pair(const T* p, float& lo, float& hi) {
 // One thread per output pixel and CB channels (grid.y splits the channels).  32-bit indexing
 // (the launcher checks B*C*H*W < 2^31).
 template <typename T, int CB>
+struct WarpGroup {  // one channel group's raw corner values
+  float r[CB][4];
+};
+
+template <typename T, int CB>
+__device__ __forceinline__ void warp_load(WarpGroup<T, CB>& g, const T* __restrict__ x,
+                                          unsigned n, int C, unsigned plane, int c0, int W,
+                                          const Pairs& kp, const Corners& kc) {
+  if (W >= 2) {
+    float lo[CB][2], hi[CB][2];
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = min(c0 + i, C - 1);
+      const T* p = x + ((unsigned)(n * C + c)) * plane;
+      load_pair(p + kp.i0, lo[i][0], hi[i][0]);
+      load_pair(p + kp.i1, lo[i][1], hi[i][1]);
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      g.r[i][0] = kp.l_lo ? lo[i][0] : hi[i][0];
+      g.r[i][1] = kp.r_lo ? lo[i][0] : hi[i][0];
+      g.r[i][2] = kp.l_lo ? lo[i][1] : hi[i][1];
+      g.r[i][3] = kp.r_lo ? lo[i][1] : hi[i][1];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = min(c0 + i, C - 1);
+      const T* p = x + ((unsigned)(n * C + c)) * plane;
+      g.r[i][0] = to_f32(p[kc.i00]);
+      g.r[i][1] = to_f32(p[kc.i01]);
+      g.r[i][2] = to_f32(p[kc.i10]);
+      g.r[i][3] = to_f32(p[kc.i11]);
+    }
+  }
+}
+
+// One thread per output pixel; grid.y splits the channels into slices of NG groups of CB
+// channels, and a thread walks its slice's groups with the next group's gathers in flight
+// while the current one is blended and stored.  32-bit indexing (the launcher checks
+// B*C*H*W < 2^31).
+template <typename T, int CB, int NG, bool XCD>
 __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ flow,
                                                        T* __restrict__ out, int B, int C, int H,
                                                        int W, float halfx, float halfy) {
   const unsigned plane = (unsigned)(H * W);
-  const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+  // XCD: consecutive pixel blocks (which gather overlapping source rows) share an L2
+  const unsigned bx = XCD ? (unsigned)xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const unsigned idx = bx * 256u + threadIdx.x;
   if (idx >= (unsigned)B * plane) return;
   const unsigned n = idx / plane;
   const unsigned pix = idx - n * plane;
@@ -144,48 +190,26 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
   const Bilinear b = bilinear(ix, iy, H, W);
   const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;  // feed fma operands: not fusable
   const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
-  const int c0 = blockIdx.y * CB;
-  float r[CB][4];
-  float m00, m01, m10, m11;
-  if (W >= 2) {
-    const Pairs k = pairs(b, H, W);
-    m00 = k.m00; m01 = k.m01; m10 = k.m10; m11 = k.m11;
-    float lo[CB][2], hi[CB][2];
+  const Pairs kp = pairs(b, H, W);
+  const Corners kc = corners(b, H, W);
+  const float m00 = kc.m00, m01 = kc.m01, m10 = kc.m10, m11 = kc.m11;
+  const int cs = blockIdx.y * CB * NG;
+  WarpGroup<T, CB> g[2];
+  warp_load(g[0], x, n, C, plane, cs, W, kp, kc);
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+    const int c0 = cs + gi * CB;
+    if (gi + 1 < NG) warp_load(g[(gi + 1) & 1], x, n, C, plane, c0 + CB, W, kp, kc);
+    const WarpGroup<T, CB>& cur = g[gi & 1];
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
-      const int c = min(c0 + i, C - 1);
-      const T* p = x + ((unsigned)(n * C + c)) * plane;
-      load_pair(p + k.i0, lo[i][0], hi[i][0]);
-      load_pair(p + k.i1, lo[i][1], hi[i][1]);
+      float acc = 0.f;
+      acc = fmaf(masked(cur.r[i][0], m00), w00, acc);
+      acc = fmaf(masked(cur.r[i][1], m01), w01, acc);
+      acc = fmaf(masked(cur.r[i][2], m10), w10, acc);
+      acc = fmaf(masked(cur.r[i][3], m11), w11, acc);
+      if (c0 + i < C) out[((unsigned)(n * C + c0 + i)) * plane + pix] = from_f32<T>(acc);
     }
-#pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      r[i][0] = k.l_lo ? lo[i][0] : hi[i][0];
-      r[i][1] = k.r_lo ? lo[i][0] : hi[i][0];
-      r[i][2] = k.l_lo ? lo[i][1] : hi[i][1];
-      r[i][3] = k.r_lo ? lo[i][1] : hi[i][1];
-    }
-  } else {
-    const Corners k = corners(b, H, W);
-    m00 = k.m00; m01 = k.m01; m10 = k.m10; m11 = k.m11;
-#pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int c = min(c0 + i, C - 1);
-      const T* p = x + ((unsigned)(n * C + c)) * plane;
-      r[i][0] = to_f32(p[k.i00]);
-      r[i][1] = to_f32(p[k.i01]);
-      r[i][2] = to_f32(p[k.i10]);
-      r[i][3] = to_f32(p[k.i11]);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < CB; ++i) {
-    float acc = 0.f;
-    acc = fmaf(masked(r[i][0], m00), w00, acc);
-    acc = fmaf(masked(r[i][1], m01), w01, acc);
-    acc = fmaf(masked(r[i][2], m10), w10, acc);
-    acc = fmaf(masked(r[i][3], m11), w11, acc);
-    if (c0 + i < C) out[((unsigned)(n * C + c0 + i)) * plane + pix] = from_f32<T>(acc);
   }
 }
 
@@ -245,17 +269,39 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   gflow[(2 * n + 1) * plane + pix] = (giy * my) / halfy;
 }
 
+// PWC_WARP_CFG=<digit> selects a (channels per group, groups per thread) variant for
+// measurement: 0 = 4 channels per thread, XCD-grouped pixel blocks (default), 1 = 8, 2 = 2,
+// 3 = 4 without XCD grouping, 4 = 2 grouped, 5 = 8 grouped.
+static int warp_cfg() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("PWC_WARP_CFG");
+    v = (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 0;
+  }
+  return v;
+}
+
 template <typename T>
 hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int C, int H,
                           int W, hipStream_t stream) {
   const size_t npix = (size_t)B * H * W;
   if (npix == 0 || C == 0) return hipSuccess;
   if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
-  constexpr int CB = 8;
   const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
-  dim3 grid((unsigned)((npix + 255) / 256), (unsigned)((C + CB - 1) / CB));
-  hipLaunchKernelGGL((warp_fwd_kernel<T, CB>), grid, dim3(256), 0, stream, (const T*)x,
-                     (const T*)flow, (T*)out, B, C, H, W, halfx, halfy);
+  const unsigned gx = (unsigned)((npix + 255) / 256);
+#define PWC_WARP_LAUNCH(CB, NG, XCD)                                                          \
+  hipLaunchKernelGGL((warp_fwd_kernel<T, CB, NG, XCD>),                                       \
+                     dim3(gx, (unsigned)((C + CB * NG - 1) / (CB * NG))), dim3(256), 0, stream, \
+                     (const T*)x, (const T*)flow, (T*)out, B, C, H, W, halfx, halfy)
+  switch (warp_cfg()) {
+    case 1: PWC_WARP_LAUNCH(8, 1, false); break;
+    case 2: PWC_WARP_LAUNCH(2, 1, false); break;
+    case 3: PWC_WARP_LAUNCH(4, 1, false); break;
+    case 4: PWC_WARP_LAUNCH(2, 1, true); break;
+    case 5: PWC_WARP_LAUNCH(8, 1, true); break;
+    default: PWC_WARP_LAUNCH(4, 1, true); break;
+  }
+#undef PWC_WARP_LAUNCH
   return hipGetLastError();
 }
 

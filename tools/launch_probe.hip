@@ -11,6 +11,19 @@ __global__ void touch(float* p, int n) {
   if (i < n) p[i] = p[i] * 0.5f + 1.f;
 }
 
+template <bool USE_LDS, bool BAR>
+__global__ void touch_v(float* p, int n) {
+  extern __shared__ float l[];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float v = (float)i;
+  if (USE_LDS) {
+    l[threadIdx.x] = v;
+    v = l[(threadIdx.x + 1) % blockDim.x];
+  }
+  if (BAR) __syncthreads();
+  if (i < n) p[i] = v;
+}
+
 __global__ void touch_lds(float* p, int n) {
   extern __shared__ float l[];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -77,20 +90,17 @@ int main() {
     (void)hipGraphExecDestroy(ge);
     (void)hipGraphDestroy(g);
   }
-  // workgroup shape / LDS / launch API variants at 288 blocks
-  hipFuncSetAttribute(reinterpret_cast<const void*>(&touch_lds),
-                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  for (int thr : {256, 512, 1024})
-    for (int ldsk : {0, 48, 96, 144}) {
-      const int n = 288 * thr;
-      const float us = time_it(s, 200, [&] {
-        hipLaunchKernelGGL(touch_lds, dim3(288), dim3(thr), ldsk * 1024 + 4096, s, p, n);
-      });
-      const float use = time_it(s, 200, [&] {
-        hipExtLaunchKernelGGL(touch_lds, dim3(288), dim3(thr), ldsk * 1024 + 4096, s, nullptr,
-                              nullptr, 0, p, n);
-      });
-      printf("288 x %4d thr, %3d KiB LDS: %.2f us (ext launch %.2f us)\n", thr, ldsk, us, use);
-    }
+  hipFuncSetAttribute(reinterpret_cast<const void*>(&touch_v<true, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  // floor of a trivial kernel vs grid size, LDS use and a workgroup barrier
+  for (int nb : {256, 288, 512, 1024}) {
+    const int n = nb * 256;
+    const float a = time_it(s, 200, [&] { hipLaunchKernelGGL((touch_v<false, false>), dim3(nb), dim3(256), 0, s, p, n); });
+    const float b = time_it(s, 200, [&] { hipLaunchKernelGGL((touch_v<false, true>), dim3(nb), dim3(256), 0, s, p, n); });
+    const float c = time_it(s, 200, [&] { hipLaunchKernelGGL((touch_v<true, false>), dim3(nb), dim3(256), 4096, s, p, n); });
+    const float d = time_it(s, 200, [&] { hipLaunchKernelGGL((touch_v<true, true>), dim3(nb), dim3(256), 4096, s, p, n); });
+    const float e = time_it(s, 200, [&] { hipLaunchKernelGGL((touch_v<true, true>), dim3(nb), dim3(256), 65536, s, p, n); });
+    printf("%4d blocks: plain %.2f | barrier %.2f | lds %.2f | lds+barrier %.2f | 64K lds+barrier %.2f us\n",
+           nb, a, b, c, d, e);
+  }
   return 0;
 }

@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int OFF>
 __device__ __forceinline__ void rd6(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
@@ -61,6 +62,27 @@ __device__ __forceinline__ void chan(const uint32_t (&ad)[6], float (&acc)[9][4]
   }
   if constexpr (MODE == 2) {
     asm volatile("" ::"v"(a), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]));
+    return;
+  }
+  if constexpr (MODE == 4 || MODE == 5) {  // packed: acc pairs += a pairs * w pairs
+    if constexpr (MODE == 5) {
+      a = keep[0];
+      for (int u = 0; u < 5; ++u) b[u] = keep[u + 1];
+    }
+#pragma unroll
+    for (int ti = 0; ti < 9; ++ti) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * h + 2 * ti;  // even
+        const f32x4 q = b[j >> 2];
+        const f32x2 w2 = (j & 2) ? f32x2{q.z, q.w} : f32x2{q.x, q.y};
+        const f32x2 a2 = h ? f32x2{a.z, a.w} : f32x2{a.x, a.y};
+        f32x2 c2 = {acc[ti][2 * h], acc[ti][2 * h + 1]};
+        c2 = __builtin_elementwise_fma(a2, w2, c2);
+        acc[ti][2 * h] = c2.x;
+        acc[ti][2 * h + 1] = c2.y;
+      }
+    }
     return;
   }
   const float av[4] = {a.x, a.y, a.z, a.w};
@@ -159,25 +181,13 @@ void run(const char* name, int waves, int bpc, int chans) {
 
 int main() {
   const int CH = 512;
-  // current structure: 9 waves, barrier every 2 channels
-  run<0, 2>("rd6+fma", 9, 1, CH);
-  run<0, 2>("rd6+fma", 9, 2, CH);
-  run<0, 8>("rd6+fma", 9, 1, CH);
-  run<0, 8>("rd6+fma", 9, 2, CH);
-  run<0, 8>("rd6+fma", 16, 1, CH);
-  run<0, 8>("rd6+fma", 4, 1, CH);
-  run<0, 8>("rd6+fma", 4, 2, CH);
-  run<0, 8>("rd6+fma", 4, 4, CH);
-  run<0, 8>("rd6+fma", 8, 2, CH);
-  run<2, 8>("rd6 only", 9, 1, CH);
-  run<2, 8>("rd6 only", 9, 2, CH);
-  run<2, 8>("rd6 only", 16, 1, CH);
-  run<3, 8>("fma only", 9, 1, CH);
-  run<3, 8>("fma only", 9, 2, CH);
-  run<3, 8>("fma only", 16, 1, CH);
-  run<3, 8>("fma only", 4, 1, CH);
-  run<1, 8>("rd4+fma", 9, 1, CH);
-  run<1, 8>("rd4+fma", 9, 2, CH);
-  run<1, 8>("rd4+fma", 16, 1, CH);
+  run<4, 2>("rd6+pkfma", 9, 1, CH);
+  run<4, 2>("rd6+pkfma", 9, 2, CH);
+  run<4, 8>("rd6+pkfma", 9, 1, CH);
+  run<4, 8>("rd6+pkfma", 9, 2, CH);
+  run<4, 32>("rd6+pkfma", 9, 1, CH);
+  run<4, 32>("rd6+pkfma", 9, 2, CH);
+  run<4, 2>("rd6+pkfma", 3, 4, CH);
+  run<4, 2>("rd6+pkfma", 3, 6, CH);
   return 0;
 }

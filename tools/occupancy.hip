@@ -52,7 +52,7 @@ int main(int argc, char** argv) {
   printf("B=%d C=%d %dx%d: %lld tiles x %d splits\n", B, C, H, W, tiles, ns);
   float* part = nullptr;
   if (maxs > 1) (void)hipMalloc(&part, (size_t)maxs * B * 81 * H * W * 4);
-  (void)hipMalloc(&g_census, nb * 16);
+  (void)hipMalloc(&g_census, nb * 32);
   for (int rep = 0; rep < 3; ++rep)
     (void)corr_forward_ring_f32(a, b, o, B, C, H, W, H, W, 0, 4, 2, 0, 32.f, maxs, part, 0);
   (void)hipDeviceSynchronize();
@@ -69,8 +69,23 @@ int main(int argc, char** argv) {
     (void)hipEventElapsedTime(&ms, e0, e1);
     printf("  back-to-back: %.2f us per launch\n", ms * 1000 / 50);
   }
-  std::vector<unsigned> h(nb * 4);
-  (void)hipMemcpy(h.data(), g_census, nb * 16, hipMemcpyDeviceToHost);
+  std::vector<unsigned> h8(nb * 8), h(nb * 4);
+  (void)hipMemcpy(h8.data(), g_census, nb * 32, hipMemcpyDeviceToHost);
+  {
+    std::vector<unsigned> pro, loop, rt;
+    for (int i = 0; i < nb; ++i) {
+      for (int k = 0; k < 4; ++k) h[i * 4 + k] = h8[i * 8 + k];
+      pro.push_back(h8[i * 8 + 4]);
+      loop.push_back(h8[i * 8 + 5]);
+      rt.push_back(h8[i * 8 + 6]);
+    }
+    std::sort(pro.begin(), pro.end());
+    std::sort(loop.begin(), loop.end());
+    std::sort(rt.begin(), rt.end());
+    printf("  prologue cycles p50 %u | stage-loop cycles p50 %u max %u | loop ticks p50 %u -> "
+           "clock %.2f GHz\n", pro[nb / 2], loop[nb / 2], loop[nb - 1], rt[nb / 2],
+           (double)loop[nb / 2] / (rt[nb / 2] * 10.0));
+  }
   int maxc = 0;
   double life = 0;
   unsigned tmin = ~0u, tmax = 0;
