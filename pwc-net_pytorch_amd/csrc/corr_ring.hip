@@ -280,15 +280,15 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     }
     __builtin_amdgcn_s_barrier();
 #endif
-#ifdef PWC_RING_ABLATION  // diagnostic build: g_ablation 1 = no FMA work, 2 = no DMA
-    if (g_ablation != 2)
+#ifdef PWC_RING_ABLATION  // diagnostic build: g_ablation bits 1 = no FMA work, 2 = no DMA
+    if (!(g_ablation & 2))
 #endif
     if (st + G::NS - 1 < nst)
       ring_issue<G>(st + G::NS - 1, c_begin, wave, plane, lds0, img1, img2, img_bytes, src_off,
                     dst_off, from_f2);
     const uint32_t sb = lds0 + (uint32_t)((st % G::NS) * G::STAGE_FLOATS) * 4u;
 #ifdef PWC_RING_ABLATION
-    if (g_ablation == 1) continue;
+    if (g_ablation & 1) continue;
 #endif
     const uint32_t addr[6] = {sb + aoff, sb + woff[0], sb + woff[1], sb + woff[2], sb + woff[3],
                               sb + woff[4]};
@@ -316,6 +316,17 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
   const int oy = oy0 + ty;
   const int ox = ox0 + 4 * q;
   if (oy >= Ho || ox >= Wo) return;
+#ifdef PWC_RING_ABLATION  // bit 4 = no output stores (results kept live through a NaN test)
+  if (g_ablation & 4) {
+    float z = 0.f;
+#pragma unroll
+    for (int a = 0; a < G::D; ++a)
+#pragma unroll
+      for (int k = 0; k < G::PX; ++k) z += acc[a][k];
+    if (z != z) out[0] = z;
+    return;
+  }
+#endif
   const int OC = G::D * G::D;
   const int tj = tj0 + tjx - G::DR;
   if (gridDim.y > 1) {  // split: raw partial sums, reduced by corr_reduce_splits
