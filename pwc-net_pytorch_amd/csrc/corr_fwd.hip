@@ -457,6 +457,11 @@ hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, in
                                  int layout, float divisor, int max_splits, void* partial,
                                  hipStream_t stream);
 
+// corr_pt.hip
+hipError_t corr_forward_pt_f32(const void* in1, const void* in2, void* out, int B, int C, int H,
+                               int W, int Ho, int Wo, int off, int dr, int s2, int layout,
+                               float divisor, int groups, hipStream_t stream);
+
 // corr_grp.hip
 hipError_t corr_forward_grp_f32(const void* in1, const void* in2, void* out, int B, int C, int H,
                                 int W, int Ho, int Wo, int off, int dr, int s2, int layout,
@@ -478,6 +483,16 @@ int corr_max_splits(int B, int OC, int Ho, int Wo) {
 size_t corr_workspace_bytes(int B, int OC, int Ho, int Wo) {
   const int k = corr_max_splits(B, OC, Ho, Wo);
   return k > 1 ? (size_t)k * B * OC * Ho * Wo * sizeof(float) : 0;
+}
+
+// PWC_CORR_PT=0 disables the parity-tile kernel (measurement of the older paths).
+static bool pt_disabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = std::getenv("PWC_CORR_PT");
+    v = (s && s[0] == '0') ? 1 : 0;
+  }
+  return v == 1;
 }
 
 // PWC_CORR_GRP=0 disables the coarse-level kernel (measurement of the split path only).
@@ -503,6 +518,13 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
   const int max_splits = workspace ? corr_max_splits(B, D * D, Ho, Wo) : 1;
   if (max_splits <= 1) workspace = nullptr;
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4) {
+    // stride-2 displacements with 16-B aligned rows (l2..l4 of PWC-Net): parity tiles
+    // (corr_pt.hip), channel groups chosen by grid size
+    if (dr == 4 && s2 == 2 && W % 4 == 0 && (md - pad) % 4 == 0 && !pt_disabled()) {
+      const hipError_t e = corr_forward_pt_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad, dr,
+                                               s2, layout, divisor, 0, stream);
+      if (e != hipErrorNotSupported) return e;
+    }
     // coarse levels (too few 16x16 tiles to fill the chip) with 16-B aligned rows:
     // in-workgroup channel groups (corr_grp.hip); unaligned rows (W % 4 != 0, the smallest
     // pyramid levels) measured faster on the channel-split path below.

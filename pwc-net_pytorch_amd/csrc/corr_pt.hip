@@ -62,35 +62,44 @@ __host__ __device__ __forceinline__ int f2_swz(int rho) {
 }
 __host__ __device__ __forceinline__ int f1_swz(int r) { return (r >> 2) & 1; }
 
-template <int CC_, int NS_, int PD_>
+// K channel groups share a workgroup of 8 waves: group g = waves g*8/K .. (g+1)*8/K - 1, each
+// wave three tile rows, so a tile is TR = 24/K parity rows.  Every stage carries CC = K*CPG
+// channels; group g accumulates channels g*CPG .. g*CPG+CPG-1 of each stage and the K partial
+// sums meet in LDS at the end (fixed order: deterministic).  K = 1 is the l4 shape; K > 1
+// trades tile rows for channel parallelism on the coarse levels (fewer, deeper pixels).
+template <int K_, int CPG_, int NS_>
 struct PtTile {
   static constexpr int DR = 4, S = 2, D = 9;
-  static constexpr int TR = 24;           // parity rows per tile
+  static constexpr int K = K_, CPG = CPG_, NS = NS_, PD = 1;
+  static constexpr int NWAVES = 8, THREADS = 64 * NWAVES;
+  static constexpr int WPG = NWAVES / K;  // waves per channel group
+  static constexpr int TR = 3 * WPG;      // parity rows per tile
   static constexpr int TX = 16;           // columns per tile: two 8-pixel segments
-  static constexpr int R2 = TR + 2 * DR;  // 32 f2 rows
+  static constexpr int R2 = TR + 2 * DR;  // f2 rows
   static constexpr int X2 = 32;           // f2 row: columns x0-8 .. x0+23
-  static constexpr int CC = CC_, NS = NS_, PD = PD_;  // PD: LDS read prefetch distance
+  static constexpr int CC = K * CPG;      // channels per stage
   static constexpr int F2_FLOATS = R2 * X2;
   static constexpr int F1_FLOATS = TR * TX;
   static constexpr int CH_FLOATS = F2_FLOATS + F1_FLOATS;
   static constexpr int CH_BYTES = CH_FLOATS * 4;
   static constexpr int STAGE_BYTES = CC * CH_BYTES;
-  static constexpr int LDS_BYTES = NS * STAGE_BYTES;
-  static constexpr int THREADS = 512;     // 8 waves x 54 lanes used
-  static constexpr int NWAVES = THREADS / 64;
-  static constexpr int PPC = 6;           // DMA pieces per channel: 4 f2 + f1 rows 0-15, 16-23
+  static constexpr int RED_BYTES = K > 1 ? 18 * THREADS * 16 : 0;  // partial sums, K > 1
+  static constexpr int RING_BYTES = NS * STAGE_BYTES;
+  static constexpr int LDS_BYTES = RING_BYTES > RED_BYTES ? RING_BYTES : RED_BYTES;
+  // DMA pieces per channel (1 KiB wave-instructions, partial EXEC on the last of each kind)
+  static constexpr int F2P = (R2 + 7) / 8;   // 8 rows x 8 quads
+  static constexpr int F1P = (TR + 15) / 16; // 16 rows x 4 quads
+  static constexpr int PPC = F2P + F1P;
   static constexpr int PIECES = CC * PPC;
-  static constexpr int ISSUERS = 8;
+  static constexpr int ISSUERS = NWAVES;
   static constexpr int PPW = PIECES / ISSUERS;
+  static_assert(K == 1 || K == 2 || K == 4 || K == 8, "channel groups");
+  static_assert(CPG % 2 == 0, "register buffers alternate by channel parity within a stage");
   static_assert(PIECES % ISSUERS == 0, "uniform DMA pieces per issuing wave");
-  static_assert(ISSUERS <= NWAVES, "issuers");
-  static_assert(NWAVES * 3 == TR, "three tile rows per wave");
-  static_assert((NS - 2) * PPW <= 63, "vmcnt range");
+  static_assert((NS - 3) * PPW <= 63, "vmcnt range");
   static_assert(NS >= 3, "ring depth: stage st+1 must be resident while st is consumed");
-  static_assert(CC == 4 && PD >= 1 && PD < CC, "four register buffers, one per channel");
-  static_assert(8 * PD <= 15, "lgkmcnt is 4 bits");
+  static_assert(8 * PD <= 15, "lgkmcnt is 4 bits: one channel of reads ahead");
   static_assert(LDS_BYTES <= 163840, "LDS");
-  static_assert((CC - 1) * CH_BYTES < 65536, "channel offset immediate");
 };
 
 // Eight ds_read_b128 into r (no wait: the caller waits with rd_wait before using r).
@@ -132,58 +141,49 @@ __device__ __forceinline__ void fma8(const f32x4 (&v)[8], float (&lo)[D][4], flo
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Channel CI of the current stage (global channel 4*st + CI uses register buffer CI % 4).
-// Reads run PD channels ahead: before the FMAs of channel CI the reads of channel CI + PD are
-// issued (into the next stage's slot once CI + PD >= CC), so PD channels of LDS latency hide
-// under the lane's own FMAs; lgkmcnt(8 * PD) then waits for channel CI only.
-template <class G, int CI, int PD>
+// Channel CI (of the group's CPG per stage) of the current stage; register buffer CI & 1.
+// The reads of the next channel (in the next stage's slot after the last) are issued before
+// the FMAs of this one, so one channel of LDS latency hides under the lane's own FMAs;
+// lgkmcnt(8) then waits for this channel's eight reads only.
+template <class G, int CI>
 __device__ __forceinline__ void pt_chan(const uint32_t (&a)[8], const uint32_t (&an)[8],
-                                        f32x4 (&buf)[4][8], float (&lo)[G::D][4],
+                                        f32x4 (&buf)[2][8], float (&lo)[G::D][4],
                                         float (&hi)[G::D][4]) {
-  if constexpr (CI < G::CC) {
-    constexpr int NC = CI + PD;
-    if constexpr (NC < G::CC)
-      rd8<NC * G::CH_BYTES>(a, buf[NC % 4]);
+  if constexpr (CI < G::CPG) {
+    if constexpr (CI + 1 < G::CPG)
+      rd8<(CI + 1) * G::CH_BYTES>(a, buf[(CI + 1) & 1]);
     else
-      rd8<(NC - G::CC) * G::CH_BYTES>(an, buf[NC % 4]);
-    rd_wait<8 * PD>(buf[CI % 4]);
-    fma8<G::D>(buf[CI % 4], lo, hi);
-    pt_chan<G, CI + 1, PD>(a, an, buf, lo, hi);
-  }
-}
-
-template <class G, int I, int PD>
-__device__ __forceinline__ void pt_prime(const uint32_t (&a)[8], f32x4 (&buf)[4][8]) {
-  if constexpr (I < PD) {
-    rd8<I * G::CH_BYTES>(a, buf[I]);
-    pt_prime<G, I + 1, PD>(a, buf);
+      rd8<0>(an, buf[(CI + 1) & 1]);
+    rd_wait<8>(buf[CI & 1]);
+    fma8<G::D>(buf[CI & 1], lo, hi);
+    pt_chan<G, CI + 1>(a, an, buf, lo, hi);
   }
 }
 
 // DMA of one stage: issuer wave w owns pieces w*PPW .. w*PPW+PPW-1 (channel p / PPC, piece
-// p % PPC).  The buffer resource's base moves to the stage's first channel (scalar work only)
-// so the per-lane voffsets are stage-invariant; channels past C read zeros because
-// num_records shrinks with the base.  Piece 5 (f1 rows 16-23) is issued by lanes 0-31 only.
+// p % PPC: f2 pieces first, then f1).  The buffer resource's base moves to the stage's first
+// channel (scalar work only) so the per-lane voffsets are stage-invariant; channels past C
+// read zeros because num_records shrinks with the base.  Lanes past a partial piece's rows
+// are masked off (their linear LDS destination would spill into the next region).
 template <class G>
-__device__ __forceinline__ void pt_issue(int stage, int wave, int lane, uint32_t plane,
-                                         uint32_t lds0, const float* img1, const float* img2,
+__device__ __forceinline__ void pt_issue(int stage, int wave, uint32_t plane, uint32_t lds0,
+                                         const float* img1, const float* img2,
                                          uint32_t img_bytes, const uint32_t (&src_off)[G::PPW],
-                                         const uint32_t (&dst_off)[G::PPW]) {
+                                         const uint32_t (&dst_off)[G::PPW], uint32_t act) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (wave >= G::ISSUERS) return;
   const uint32_t cbytes = (uint32_t)(stage * G::CC) * plane * 4u;
   const int nrec = cbytes < img_bytes ? (int)(img_bytes - cbytes) : 0;
   const uint32_t sbase = lds0 + (uint32_t)(stage % G::NS) * (uint32_t)G::STAGE_BYTES;
 #pragma unroll
   for (int i = 0; i < G::PPW; ++i) {
     const int k = (wave * G::PPW + i) % G::PPC;  // wave-uniform
-    const uint64_t b = (uint64_t)(uintptr_t)(k < 4 ? img2 : img1) + (uint64_t)cbytes;
+    const uint64_t b = (uint64_t)(uintptr_t)(k < G::F2P ? img2 : img1) + (uint64_t)cbytes;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
         __builtin_amdgcn_readfirstlane(nrec), 0x00020000);
-    if (k != 5 || lane < 32)
+    if ((act >> i) & 1)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs, (__attribute__((address_space(3))) void*)(uintptr_t)(sbase + dst_off[i]), 16,
           src_off[i], 0, 0, 0);
@@ -214,17 +214,18 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // lane -> (tj, r, s): wave w owns rows 3w .. 3w+2 of the tile, all nine tj, both 8-pixel
-  // segments (54 lanes; s fastest, then row, then tj).  Lanes 54..63 mirror lanes 44..53
-  // (identical addresses: LDS broadcasts) and store nothing.  Every ds_read_b128 lane group
-  // then hits 16 distinct 16-B slots or repeats an address (checked exhaustively for the
-  // swizzles below, all window quads u and both f1 quads).  Eight equal waves = two per SIMD:
-  // with seven, one SIMD held a lone wave, which issues VALU at half rate and set the pace of
-  // the whole workgroup through the stage barriers.
+  const int grp = wave / G::WPG;  // channel group
+  const int wj = wave % G::WPG;   // wave inside the group: tile rows 3wj .. 3wj+2
+  // lane -> (tj, r, s): 54 lanes = 9 tj x 3 rows x 2 eight-pixel segments (s fastest, then
+  // row, then tj).  Lanes 54..63 mirror lanes 44..53 (identical addresses: LDS broadcasts)
+  // and store nothing.  Every ds_read_b128 lane group then hits 16 distinct 16-B slots or
+  // repeats an address (checked exhaustively for the swizzles above, all window quads and
+  // both f1 quads).  Eight waves = two per SIMD: with an odd count one SIMD holds a lone
+  // wave, which issues VALU at half rate.
   const bool valid = lane < 54;
   const int ll = valid ? lane : lane - 10;
   const int tj = ll / 6;
-  const int r = 3 * wave + (ll % 6) / 2;
+  const int r = 3 * wj + (ll % 6) / 2;
   const int s = ll & 1;
 
   const uint32_t plane = (uint32_t)(H * W);
@@ -233,45 +234,49 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
   const float* img2 = in2 + (size_t)n * C * plane;
   const uint32_t lds0 = lds_addr(lds);
 
-  // ---- DMA plan (issuer waves): source byte offset for channel 0 (or OOB), LDS offset ----
+  // ---- DMA plan: source byte offset for channel 0 (or OOB), LDS offset, active lanes ----
   uint32_t src_off[G::PPW];
   uint32_t dst_off[G::PPW];
+  uint32_t act = 0;
   constexpr uint32_t kOOB = 0x80000000u;  // >= num_records: the buffer unit returns zeros
-  if (wave < G::ISSUERS) {
 #pragma unroll
-    for (int i = 0; i < G::PPW; ++i) {
-      const int pc = wave * G::PPW + i;
-      const int cc = pc / G::PPC;
-      const int k = pc % G::PPC;
-      uint32_t dst = (uint32_t)(cc * G::CH_BYTES);
-      int gy, gx;
-      if (k < 4) {
-        const int rho = 8 * k + (lane >> 3);
-        const int q = (lane & 7) ^ f2_swz(rho);
-        gy = 2 * (R0 + rho - G::DR) + p + off;
-        gx = x0 + off - 2 * G::DR + 4 * q;
-        dst += (uint32_t)(8 * k * G::X2) * 4u;
-      } else {
-        const int rr = (k == 4 ? 0 : 16) + ((lane >> 2) & 15);
-        const int q = (lane & 3) ^ f1_swz(rr);
-        gy = 2 * (R0 + rr) + p + off;
-        gx = x0 + off + 4 * q;
-        dst += (uint32_t)(G::F2_FLOATS + (k == 4 ? 0 : 16 * G::TX)) * 4u;
-      }
-      const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
-      src_off[i] = ok ? ((uint32_t)cc * plane + (uint32_t)(gy * W + gx)) * 4u : kOOB;
-      dst_off[i] = dst;
+  for (int i = 0; i < G::PPW; ++i) {
+    const int pc = wave * G::PPW + i;
+    const int cc = pc / G::PPC;
+    const int k = pc % G::PPC;
+    uint32_t dst = (uint32_t)(cc * G::CH_BYTES);
+    int gy, gx;
+    bool on;
+    if (k < G::F2P) {
+      const int rho = 8 * k + (lane >> 3);
+      const int q = (lane & 7) ^ f2_swz(rho);
+      on = rho < G::R2;
+      gy = 2 * (R0 + rho - G::DR) + p + off;
+      gx = x0 + off - 2 * G::DR + 4 * q;
+      dst += (uint32_t)(8 * k * G::X2) * 4u;
+    } else {
+      const int rr = 16 * (k - G::F2P) + (lane >> 2);
+      const int q = (lane & 3) ^ f1_swz(rr);
+      on = rr < G::TR;
+      gy = 2 * (R0 + rr) + p + off;
+      gx = x0 + off + 4 * q;
+      dst += (uint32_t)(G::F2_FLOATS + 16 * (k - G::F2P) * G::TX) * 4u;
     }
+    const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
+    src_off[i] = ok ? ((uint32_t)cc * plane + (uint32_t)(gy * W + gx)) * 4u : kOOB;
+    dst_off[i] = dst;
+    act |= (on ? 1u : 0u) << i;
   }
 
-  // ---- lane-constant LDS read offsets (bytes inside a channel block) ----
+  // ---- lane-constant LDS read offsets (bytes from the stage slot; group's channel block) ----
   const int rho = r + tj;
+  const uint32_t gbase = (uint32_t)(grp * G::CPG * G::CH_BYTES);
   uint32_t off8[8];
-  off8[0] = (uint32_t)(G::F2_FLOATS + r * G::TX + (((2 * s) ^ f1_swz(r)) << 2)) * 4u;
-  off8[1] = (uint32_t)(G::F2_FLOATS + r * G::TX + (((2 * s + 1) ^ f1_swz(r)) << 2)) * 4u;
+  off8[0] = gbase + (uint32_t)(G::F2_FLOATS + r * G::TX + (((2 * s) ^ f1_swz(r)) << 2)) * 4u;
+  off8[1] = gbase + (uint32_t)(G::F2_FLOATS + r * G::TX + (((2 * s + 1) ^ f1_swz(r)) << 2)) * 4u;
 #pragma unroll
   for (int u = 0; u < 6; ++u)
-    off8[2 + u] = (uint32_t)(rho * G::X2 + (((2 * s + u) ^ f2_swz(rho)) << 2)) * 4u;
+    off8[2 + u] = gbase + (uint32_t)(rho * G::X2 + (((2 * s + u) ^ f2_swz(rho)) << 2)) * 4u;
 
   float lo[G::D][4], hi[G::D][4];
 #pragma unroll
@@ -283,14 +288,14 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
 #pragma unroll
   for (int st = 0; st < G::NS - 1; ++st)
     if (st < nst)
-      pt_issue<G>(st, wave, lane, plane, lds0, img1, img2, img_bytes, src_off, dst_off);
+      pt_issue<G>(st, wave, plane, lds0, img1, img2, img_bytes, src_off, dst_off, act);
 
   // Stage st is consumed with stage st+1 already resident (the reads run into it), so the
   // barrier at the top of stage st waits for stage st+1's DMA; it also releases the slot of
   // stage st-1, which all waves have finished reading, to the DMA of stage st+NS-1.
-  f32x4 buf[4][8];
+  f32x4 buf[2][8];
   for (int st = 0; st < nst; ++st) {
-    if (wave < G::ISSUERS) {
+    {
       // issued so far: stages 0 .. min(nst, st+NS-1)-1; keep all but stages <= st+1 in flight
       const int issued = min(nst, st + G::NS - 1);
       if (issued - (st + 2) >= G::NS - 3)
@@ -303,8 +308,8 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
     if (!(g_pt_abl & 2))
 #endif
     if (st + G::NS - 1 < nst)
-      pt_issue<G>(st + G::NS - 1, wave, lane, plane, lds0, img1, img2, img_bytes, src_off,
-                  dst_off);
+      pt_issue<G>(st + G::NS - 1, wave, plane, lds0, img1, img2, img_bytes, src_off, dst_off,
+                  act);
 #ifdef PWC_PT_ABLATION
     if (g_pt_abl & 1) continue;
 #endif
@@ -316,16 +321,16 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
       a[u] = sb + off8[u];
       an[u] = sn + off8[u];
     }
-    if (st == 0) pt_prime<G, 0, G::PD>(a, buf);
-    pt_chan<G, 0, G::PD>(a, an, buf, lo, hi);
+    if (st == 0) rd8<0>(a, buf[0]);
+    pt_chan<G, 0>(a, an, buf, lo, hi);
   }
-  // the last PD prefetches read a slot past the data (discarded): drain them before exit
+  // the last prefetch read a slot past the data (discarded): drain it
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   // ---- epilogue: out = acc / divisor (cu:100); a power-of-two divisor is an exact scale ----
   const int oy = 2 * (R0 + r) + p;
   const int ox = x0 + 8 * s;
-  if (!valid || oy >= Ho || ox >= Wo) return;
+  const bool st_ok = valid && oy < Ho && ox < Wo;
 #ifdef PWC_PT_ABLATION
   if (g_pt_abl & 4) {
     float z = 0.f;
@@ -340,24 +345,44 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
   const int OC = G::D * G::D;
   const bool pow2 = inv_divisor != 0.f;
   const bool has_hi = ox + 4 < Wo;
-#pragma unroll
-  for (int ti = 0; ti < G::D; ++ti) {
+  float* obase = out + (((size_t)n * OC) * Ho + oy) * Wo + ox;
+  auto emit = [&](int v, f32x4 q) {  // v = 2*ti + h
+    const int ti = v >> 1, h = v & 1;
+    if (!st_ok || (h && !has_hi)) return;
     const int oc = out_channel(layout, tj - G::DR, ti - G::DR, G::DR, G::D, G::S);
-    float* orow = out + (((size_t)n * OC + oc) * Ho + oy) * Wo + ox;
-    float4 v0, v1;
-    if (pow2) {
-      v0 = make_float4(lo[ti][0] * inv_divisor, lo[ti][1] * inv_divisor,
-                       lo[ti][2] * inv_divisor, lo[ti][3] * inv_divisor);
-      v1 = make_float4(hi[ti][0] * inv_divisor, hi[ti][1] * inv_divisor,
-                       hi[ti][2] * inv_divisor, hi[ti][3] * inv_divisor);
-    } else {
-      v0 = make_float4(lo[ti][0] / divisor, lo[ti][1] / divisor, lo[ti][2] / divisor,
-                       lo[ti][3] / divisor);
-      v1 = make_float4(hi[ti][0] / divisor, hi[ti][1] / divisor, hi[ti][2] / divisor,
-                       hi[ti][3] / divisor);
+    if (pow2)
+      q *= inv_divisor;
+    else
+      q /= divisor;
+    *reinterpret_cast<f32x4*>(obase + (size_t)oc * Ho * Wo + 4 * h) = q;
+  };
+  if constexpr (G::K == 1) {
+#pragma unroll
+    for (int ti = 0; ti < G::D; ++ti) {
+      emit(2 * ti, f32x4{lo[ti][0], lo[ti][1], lo[ti][2], lo[ti][3]});
+      emit(2 * ti + 1, f32x4{hi[ti][0], hi[ti][1], hi[ti][2], hi[ti][3]});
     }
-    *reinterpret_cast<float4*>(orow) = v0;
-    if (has_hi) *reinterpret_cast<float4*>(orow + 4) = v1;
+  } else {
+    // K partial sums per output: every lane parks its 18 float4 in LDS ([v][group][slot],
+    // 16-B consecutive per lane: conflict-free), then group g finalises slots v == g mod K as
+    // ((p_0 + p_1) + p_2) + ... in group order and stores them.
+    __builtin_amdgcn_s_barrier();  // every wave is past its last ring read
+    f32x4* red = reinterpret_cast<f32x4*>(lds);
+    const int slot = wj * 64 + lane;  // the same output item in every group
+#pragma unroll
+    for (int v = 0; v < 18; ++v) {
+      const int ti = v >> 1;
+      const f32x4 q = (v & 1) ? f32x4{hi[ti][0], hi[ti][1], hi[ti][2], hi[ti][3]}
+                              : f32x4{lo[ti][0], lo[ti][1], lo[ti][2], lo[ti][3]};
+      red[(v * G::K + grp) * (G::WPG * 64) + slot] = q;
+    }
+    __syncthreads();
+    for (int v = grp; v < 18; v += G::K) {
+      f32x4 q = red[(v * G::K) * (G::WPG * 64) + slot];
+#pragma unroll
+      for (int g = 1; g < G::K; ++g) q += red[(v * G::K + g) * (G::WPG * 64) + slot];
+      emit(v, q);
+    }
   }
 }
 
@@ -389,37 +414,45 @@ static hipError_t launch_pt(const void* in1, const void* in2, void* out, int B, 
   return hipGetLastError();
 }
 
-// (lgkmcnt is 4 bits on gfx950: with 8 reads per channel only one channel can be in flight
-// ahead of the one being consumed, PD = 1)
-using PtA = PtTile<4, 7, 1>;  // 154 KiB: stages st+1 .. st+5 in flight
-using PtB = PtTile<4, 6, 1>;  // 132 KiB: stages st+1 .. st+4 in flight
-using PtC = PtTile<4, 5, 1>;  // 110 KiB: stages st+1 .. st+3 in flight
-
-static int pt_cfg() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = std::getenv("PWC_PT_CFG");
-    v = 0;
-    if (s && s[0] >= 'A' && s[0] <= 'C' && s[1] == 0) v = s[0] - 'A';
-  }
-  return v;
-}
+//                   K  CPG NS    tile rows  stage    ring
+using Pt1 = PtTile<1, 4, 5>;   // 24       22 KiB   110 KiB: stages st+1 .. st+3 in flight
+using Pt2 = PtTile<2, 2, 12>;  // 12       13 KiB   156 KiB
+using Pt4 = PtTile<4, 2, 9>;   //  6       17 KiB   153 KiB
+using Pt8 = PtTile<8, 2, 6>;   //  3       25 KiB   150 KiB
 
 }  // namespace pt
 
-// hipErrorNotSupported: shape / alignment outside what the parity-tile kernel handles.
+// Parity-tile correlation (stride-2 displacements, dr = 4) with `groups` channel groups per
+// workgroup (1, 2, 4 or 8; 0 = pick by grid size).  hipErrorNotSupported: shape / alignment
+// outside what the kernel handles.
 hipError_t corr_forward_pt_f32(const void* in1, const void* in2, void* out, int B, int C, int H,
                                int W, int Ho, int Wo, int off, int dr, int s2, int layout,
-                               float divisor, hipStream_t stream) {
+                               float divisor, int groups, hipStream_t stream) {
   if (!(dr == 4 && s2 == 2)) return hipErrorNotSupported;
   if (W % 4 || Wo % 4 || off % 4) return hipErrorNotSupported;
   if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16)
     return hipErrorNotSupported;
   if ((size_t)C * H * W * 4 >= 0x7ffffff0ull) return hipErrorNotSupported;
-  switch (pt::pt_cfg()) {
-    case 1: return pt::launch_pt<pt::PtB>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
-    case 2: return pt::launch_pt<pt::PtC>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
-    default: return pt::launch_pt<pt::PtA>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+  if (const char* e = std::getenv("PWC_PT_K")) groups = std::atoi(e);
+  if (groups <= 0) {
+    // the largest tile (fewest halo bytes per output) that still gives ~one tile per CU;
+    // grids that fill the chip with single-group tiles stay on corr_ring.hip (measured equal
+    // or faster at l4 inside the bench's graph, where the warp has just written input2)
+    const int hp = (Ho + 1) / 2, ntx = (Wo + 15) / 16;
+    groups = 8;
+    for (int k : {1, 2, 4}) {
+      const long long tiles = (long long)B * 2 * ((hp + 24 / k - 1) / (24 / k)) * ntx;
+      if (tiles >= 192) { groups = k; break; }
+    }
+    static const bool l4 = std::getenv("PWC_PT_L4") && std::getenv("PWC_PT_L4")[0] == '1';
+    if (groups == 1 && !l4) return hipErrorNotSupported;
+  }
+  switch (groups) {
+    case 1: return pt::launch_pt<pt::Pt1>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    case 2: return pt::launch_pt<pt::Pt2>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    case 4: return pt::launch_pt<pt::Pt4>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    case 8: return pt::launch_pt<pt::Pt8>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);
+    default: return hipErrorNotSupported;
   }
 }
 

@@ -22,6 +22,7 @@
 #include "../pwc-net_pytorch_amd/csrc/corr_par.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_ring.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_pt.hip"
+#include "../pwc-net_pytorch_amd/csrc/corr_grp.hip"
 
 namespace pwc {
 hipEvent_t g_e0 = nullptr, g_e1 = nullptr;
@@ -366,13 +367,17 @@ int main(int argc, char** argv) {
                                        divisor, 0);
     }, abl == 0, 0, abl);
   }
-  const char* pt_env = std::getenv("PWC_PT_CFG");
+  run("grp", [&](const Set& s) {
+    return pwc::corr_forward_grp_f32(s.f1, s.f2, s.out, B, C, H, W, Ho, Wo, off, 4, 2, 0,
+                                     divisor, 0);
+  }, true, 0, 0);
+  const char* pt_env = std::getenv("PWC_PT_K");
   for (int abl : {0, 1, 2, 4, 5, 6, 3}) {
-    std::string nm = std::string("pt") + (pt_env ? pt_env : "A") +
+    std::string nm = std::string("pt") + (pt_env ? pt_env : "auto") +
                      (abl ? "_abl" + std::to_string(abl) : "");
     run(nm.c_str(), [&](const Set& s) {
       return pwc::corr_forward_pt_f32(s.f1, s.f2, s.out, B, C, H, W, Ho, Wo, off, 4, 2, 0,
-                                      divisor, 0);
+                                      divisor, 0, 0);
     }, abl == 0, 0, abl);
   }
   std::printf("done\n");

@@ -17,29 +17,30 @@ __global__ __launch_bounds__(512) void dma(const float* src, size_t chunk, int m
 #if defined(__HIP_DEVICE_COMPILE__)
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wg = mode == 2 ? blockIdx.x / 2 : mode == 4 ? 0 : blockIdx.x;
+  const int m = mode & 7;
+  const int wg = m == 2 ? blockIdx.x / 2 : m == 4 ? 0 : blockIdx.x;
   const char* base = (const char*)src + (size_t)wg * (1u << 20);
   const int slots = (int)(chunk / 16384);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 1 << 20, 0x00020000);
   auto voff = [&](int slot, int piece) -> uint32_t {
     const uint32_t pb = (uint32_t)slot * 16384u + (uint32_t)piece * 1024u;
-    if (mode == 1)  // piece = 8 rows of 128 B at pitch 448, starting 64 B into a line
+    if (m == 1)  // piece = 8 rows of 128 B at pitch 448, starting 64 B into a line
       return (pb / 1024) * 8 * 448 + (lane >> 3) * 448 + 64 + (lane & 7) * 16;  // < 1 MiB
-    if (mode == 5)  // 8 rows of 128 B at pitch 512: line-aligned segments
+    if (m == 5)  // 8 rows of 128 B at pitch 512: line-aligned segments
       return (pb / 1024) * 8 * 512 + (lane >> 3) * 512 + (lane & 7) * 16;
-    if (mode == 6)  // 16 rows of 64 B at pitch 448 (f1-like half lines)
+    if (m == 6)  // 16 rows of 64 B at pitch 448 (f1-like half lines)
       return (pb / 1024) * 16 * 448 + (lane >> 2) * 448 + (lane & 3) * 16;
-    if (mode == 7)  // 8 rows of 128 B at pitch 448, 32 B into the row (the f2 window shape)
+    if (m == 7)  // 8 rows of 128 B at pitch 448, 32 B into the row (the f2 window shape)
       return (pb / 1024) * 8 * 448 + (lane >> 3) * 448 + 32 + (lane & 7) * 16;
-    if (mode == 4) return (pb + lane * 16) & ((1u << 18) - 1);  // every WG: the same 256 KiB
+    if (m == 4) return (pb + lane * 16) & ((1u << 18) - 1);  // every WG: the same 256 KiB
     return pb + lane * 16;
   };
   auto issue = [&](int slot) {
     for (int i = 0; i < 2; ++i) {
       const int piece = wave * 2 + i;
       const uint32_t dst = lds0 + (uint32_t)(slot % NS) * 16384u + piece * 1024u;
-      if (mode == 3) {
+      if (m == 3) {
         const uint32_t o = voff(slot, piece);
         const float4 v = o < (1u << 20) ? *(const float4*)(base + o) : make_float4(0, 0, 0, 0);
         *(float4*)((char*)lds + (dst - lds0) + lane * 16) = v;
@@ -51,10 +52,10 @@ __global__ __launch_bounds__(512) void dma(const float* src, size_t chunk, int m
   for (int s = 0; s < NS - 1 && s < slots; ++s) issue(s);
   float acc = 0.f;
   for (int s = 0; s < slots; ++s) {
-    if (mode != 3) {
+    if (m != 3) {
       if (slots - 1 - s >= NS - 2) vm<(NS - 2) * 2>(); else vm<0>();
     }
-    __syncthreads();
+    if (!(mode & 8)) __syncthreads();
     if (s + NS - 1 < slots) issue(s + NS - 1);
     acc += lds[(s % NS) * 4096 + threadIdx.x];
   }
@@ -71,9 +72,9 @@ int main() {
   (void)hipMemset(src, 0, (size_t)nwg * (1u << 20) * 4);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-  for (int mode = 0; mode < 8; ++mode) {
+  for (int mode : {0, 4, 8, 12, 7, 15}) {
     if (hipGetLastError() != hipSuccess) return 1;
-    for (int ns : {8}) {
+    for (int ns : {4, 8}) {
       (void)hipFuncSetAttribute((const void*)dma<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 16384);
       (void)hipFuncSetAttribute((const void*)dma<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 16384);
       float best = 1e9, sum = 0;
