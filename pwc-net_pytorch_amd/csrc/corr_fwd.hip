@@ -462,6 +462,12 @@ hipError_t corr_forward_pt_f32(const void* in1, const void* in2, void* out, int 
                                int W, int Ho, int Wo, int off, int dr, int s2, int layout,
                                float divisor, int groups, hipStream_t stream);
 
+// corr_small.hip
+hipError_t corr_forward_small_f32(const void* in1, const void* in2, void* out, int B, int C,
+                                  int H, int W, int Ho, int Wo, int off, int dr, int s2,
+                                  int layout, float divisor, int max_splits, void* partial,
+                                  hipStream_t stream);
+
 // corr_grp.hip
 hipError_t corr_forward_grp_f32(const void* in1, const void* in2, void* out, int B, int C, int H,
                                 int W, int Ho, int Wo, int off, int dr, int s2, int layout,
@@ -523,6 +529,14 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
     if (dr == 4 && s2 == 2 && W % 4 == 0 && (md - pad) % 4 == 0 && !pt_disabled()) {
       const hipError_t e = corr_forward_pt_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad, dr,
                                                s2, layout, divisor, 0, stream);
+      if (e != hipErrorNotSupported) return e;
+    }
+    // the smallest levels (l0, l1: a few hundred pixels, unaligned rows): whole parity halves
+    // per workgroup, channel slices over the workspace (corr_small.hip)
+    if (dr == 4 && s2 == 2 && 9 * ((Ho + 1) / 2) * ((Wo + 7) / 8) <= 256 && !pt_disabled()) {
+      const hipError_t e = corr_forward_small_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad,
+                                                  dr, s2, layout, divisor, max_splits,
+                                                  workspace, stream);
       if (e != hipErrorNotSupported) return e;
     }
     // coarse levels (too few 16x16 tiles to fill the chip) with 16-B aligned rows:

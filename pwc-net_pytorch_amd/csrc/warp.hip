@@ -276,7 +276,7 @@ static int warp_cfg() {
   static int v = -1;
   if (v < 0) {
     const char* e = std::getenv("PWC_WARP_CFG");
-    v = (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 0;
+    v = (e && e[0] >= '0' && e[0] <= '9' && e[1] == 0) ? e[0] - '0' : 0;
   }
   return v;
 }
@@ -299,6 +299,10 @@ hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int
     case 3: PWC_WARP_LAUNCH(4, 1, false); break;
     case 4: PWC_WARP_LAUNCH(2, 1, true); break;
     case 5: PWC_WARP_LAUNCH(8, 1, true); break;
+    case 6: PWC_WARP_LAUNCH(4, 2, true); break;
+    case 7: PWC_WARP_LAUNCH(4, 4, true); break;
+    case 8: PWC_WARP_LAUNCH(4, 8, true); break;
+    case 9: PWC_WARP_LAUNCH(2, 4, true); break;
     default: PWC_WARP_LAUNCH(4, 1, true); break;
   }
 #undef PWC_WARP_LAUNCH

@@ -23,6 +23,7 @@
 #include "../pwc-net_pytorch_amd/csrc/corr_ring.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_pt.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_grp.hip"
+#include "../pwc-net_pytorch_amd/csrc/corr_small.hip"
 
 namespace pwc {
 hipEvent_t g_e0 = nullptr, g_e1 = nullptr;
@@ -31,8 +32,18 @@ void take_launch_events(hipEvent_t* a, hipEvent_t* b) {
   *b = g_e1;
   g_e0 = g_e1 = nullptr;
 }
-hipError_t corr_reduce_splits_f32(const void*, void*, size_t, int, float, float, hipStream_t) {
-  return hipErrorNotSupported;
+__global__ void red_k(const float* partial, float* out, size_t n, int nsplit, float div) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = partial[i];
+  for (int k = 1; k < nsplit; ++k) s += partial[(size_t)k * n + i];
+  out[i] = s / div;
+}
+hipError_t corr_reduce_splits_f32(const void* partial, void* out, size_t n, int nsplit,
+                                  float divisor, float, hipStream_t stream) {
+  hipLaunchKernelGGL(red_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     (const float*)partial, (float*)out, n, nsplit, divisor);
+  return hipGetLastError();
 }
 }  // namespace pwc
 
@@ -215,6 +226,8 @@ int main(int argc, char** argv) {
   }
   float* ref;
   CK(hipMalloc(&ref, nout * 4));
+  float* wsp;
+  CK(hipMalloc(&wsp, nout * 4 * 16));
   ref_corr<<<(nout + 255) / 256, 256>>>(sets[0].f1, sets[0].f2, ref, B, C, H, W, Ho, Wo, off,
                                        divisor);
   CK(hipDeviceSynchronize());
@@ -235,6 +248,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::g_ablation), &ring_abl, sizeof(int)));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::par::g_par_abl), &par_abl, sizeof(int)));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::pt::g_pt_abl), &par_abl, sizeof(int)));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::sm::g_sm_abl), &par_abl, sizeof(int)));
     if (check) {
       CK(hipMemset(sets[0].out, 0xff, nout * 4));
       CK(fn(sets[0]));
@@ -255,7 +269,13 @@ int main(int argc, char** argv) {
     for (int i = 0; i < iters; ++i) {
       pwc::g_e0 = e0[i];
       pwc::g_e1 = e1[i];
+      const bool wrap = false;  // (multi-kernel paths: the launcher times its main kernel)
+      if (wrap) {
+        pwc::g_e0 = pwc::g_e1 = nullptr;
+        CK(hipEventRecord(e0[i], 0));
+      }
       CK(fn(sets[i % nsets]));
+      if (wrap) CK(hipEventRecord(e1[i], 0));
     }
     CK(hipDeviceSynchronize());
     std::vector<float> t(iters);
@@ -365,6 +385,13 @@ int main(int argc, char** argv) {
     run(nm.c_str(), [&](const Set& s) {
       return pwc::corr_forward_par_f32(s.f1, s.f2, s.out, B, C, H, W, Ho, Wo, off, 4, 2, 0,
                                        divisor, 0);
+    }, abl == 0, 0, abl);
+  }
+  for (int abl : {0, 1, 2, 4, 7, 8}) {
+    std::string nm = std::string("small") + (abl ? "_abl" + std::to_string(abl) : "");
+    run(nm.c_str(), [&](const Set& s) {
+      return pwc::corr_forward_small_f32(s.f1, s.f2, s.out, B, C, H, W, Ho, Wo, off, 4, 2, 0,
+                                         divisor, 16, wsp, 0);
     }, abl == 0, 0, abl);
   }
   run("grp", [&](const Set& s) {
