@@ -61,7 +61,7 @@ template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_small(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
     float* __restrict__ partial, int B, int C, int H, int W, int Ho, int Wo, int off, int layout,
-    float divisor, float inv_divisor, int cps, SmGeo g) {
+    float divisor, float inv_divisor, int cps, int chk, SmGeo g) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (SM_ABL(8)) return;
   const int unit = blockIdx.x;  // (n, p); grid.y = channel slice
@@ -70,58 +70,67 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_small(
   const int c0 = slice * cps;
   const int cu = min(C, c0 + cps) - c0;  // channels of this slice
   const size_t plane = (size_t)H * W;
-#if defined(__HIP_DEVICE_COMPILE__)
   const float* f1n = in1 + ((size_t)n * C + c0) * plane;
   const float* f2n = in2 + ((size_t)n * C + c0) * plane;
-#endif
 
-  // ---- stage the slice with LDS-DMA (buffer_load_dword ... lds): job = one LDS row (f2 rows,
-  // then f1 rows, of a channel), one wave per job, lane = column.  The DMA writes lane i's
-  // dword at the row base + 4i, elements outside the image read 0 through the buffer range
-  // check, lanes past the row width are masked off.  Every job of the wave is issued before
-  // the one wait: the whole slice is in flight at once (one memory round trip). ----
-#if defined(__HIP_DEVICE_COMPILE__)
-  {
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
-    const int rpc = g.hp + 8 + g.hp;  // LDS rows per channel
-    const int njobs = cu * rpc;
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds;
-    const uint32_t nrec = (uint32_t)(cu * plane * 4);
-    const __amdgpu_buffer_rsrc_t r1 =
-        __builtin_amdgcn_make_buffer_rsrc((void*)f1n, (short)0, (int)nrec, 0x00020000);
-    const __amdgpu_buffer_rsrc_t r2 =
-        __builtin_amdgcn_make_buffer_rsrc((void*)f2n, (short)0, (int)nrec, 0x00020000);
-    // wave wv takes LDS rows rr = wv, wv + 8, ... of every channel; per row the source offset,
-    // validity and LDS base are computed once, and per channel only a vector add and a
-    // scalar add remain (the scalar unit is shared by the CU's waves: per-job integer
-    // division there cost ~10 us)
-    (void)njobs;
-    for (int rr = wv; rr < rpc; rr += 8) {
-      const bool is2 = rr < g.hp + 8;
-      const int width = is2 ? g.x2 : g.f1x;
-      const int gy = is2 ? 2 * (rr - G::DR) + p + off : 2 * (rr - g.hp - 8) + p + off;
-      const int gx = ln - (is2 ? 2 * G::DR : 0) + off;
-      const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W && !SM_ABL(1);
-      const uint32_t vo0 = (uint32_t)((gy * W + gx) * 4);
-      const uint32_t pl4 = (uint32_t)(plane * 4);
-      uint32_t row = lds0 + (uint32_t)(is2 ? rr * g.x2 : g.f2f + (rr - g.hp - 8) * g.f1x) * 4u;
-      const __amdgpu_buffer_rsrc_t rs = is2 ? r2 : r1;
-      if (ln < width) {
-        for (int cl = 0; cl < cu; ++cl) {
-          const uint32_t vo = ok ? vo0 + (uint32_t)cl * pl4 : 0x80000000u;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rs, (__attribute__((address_space(3))) void*)(uintptr_t)row, 4, vo, 0, 0, 0);
-          row += (uint32_t)g.chf * 4u;
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-#endif
-  __syncthreads();
-
-  // ---- compute: group grp takes slice channels grp, grp + K, ... ----
+  // ---- channels stream through two LDS buffers of `chk` channels (LDS-DMA, buffer_load_dword
+  // ... lds): job = one LDS row (f2 rows, then f1 rows, of a channel), wave wv takes rows
+  // rr = wv, wv + 8, ..., lane = column; the DMA writes lane i's dword at the row base + 4i,
+  // elements outside the image read 0 through the buffer range check, lanes past the row
+  // width are masked off.  All of a chunk's rows are in flight at once, and chunk c+1 loads
+  // while chunk c is consumed.  (Per-row setup, then one vector add + one scalar add per
+  // channel: the scalar unit is shared by the CU's waves, and per-job integer division there
+  // cost ~10 us.) ----
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rpc = g.hp + 8 + g.hp;  // LDS rows per channel
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds;
+  const int nchunk = (cu + chk - 1) / chk;
+  (void)rpc; (void)lds0;
+  // Register staging of the in-image elements only (off == 0, checked by the launcher): thread
+  // t owns within-channel element w = t % E of channels t / E, t / E + 512 / E, ... (E = the
+  // 2 * rows * W elements of one channel's parity half), so the element -> LDS mapping is
+  // computed once; the halo rows / columns stay zero from the initial clear and are never
+  // written again.  One batch of loads per chunk (all in flight), then the LDS writes.
+  const int hpp = (Ho - p + 1) / 2;           // parity rows that exist
+  const int E = 2 * hpp * W;                  // in-image elements per channel
+  const int cpt = E > 0 ? G::THREADS / E : 0;  // channels per pass of the block
+  const int w = E > 0 ? (int)threadIdx.x % E : 0, cofs = E > 0 ? (int)threadIdx.x / E : cpt;
+  int gsrc = 0, ldst = 0;
+  bool is1 = false;
+  if (E > 0) {
+    const int half = hpp * W;
+    is1 = w >= half;
+    const int e = is1 ? w - half : w;
+    const int r = e / W, x = e - r * W;
+    gsrc = (2 * r + p) * W + x;
+    ldst = is1 ? g.f2f + r * g.f1x + x : (r + G::DR) * g.x2 + x + 2 * G::DR;
+  }
+  const bool act = cofs < cpt;
+  {  // clear both chunk buffers (halo zeros)
+    f32x4* z = reinterpret_cast<f32x4*>(lds);
+    const int nq = (2 * chk * g.chf) >> 2;
+    for (int i = threadIdx.x; i < nq; i += G::THREADS) z[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  auto stage = [&](int chunk) {
+    const int cb = chunk * chk, ce = min(cu, cb + chk);
+    float* buf = lds + (chunk & 1) * chk * g.chf;
+    constexpr int MAXP = 32;
+    float v[MAXP];
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const int c = cb + cofs + i * cpt;
+      if (act && c < ce && !SM_ABL(1))
+        v[i] = (is1 ? f1n : f2n)[(size_t)c * plane + gsrc];
+    }
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const int c = cb + cofs + i * cpt;
+      if (act && c < ce) buf[(c - cb) * g.chf + ldst] = SM_ABL(1) ? 0.f : v[i];
+    }
+  };
+
+  // ---- compute: group grp takes chunk channels grp, grp + K, ... ----
   const int grp = wave / G::WPG;
   const int item = (wave % G::WPG) * 64 + lane;
   const int per_tj = g.hp * g.nseg;
@@ -141,14 +150,21 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_small(
   const int f1q = (g.f2f + r * g.f1x + 8 * s) >> 2;  // quad index of the lane's f1 quads
   const int f2q = (rho * g.x2 + 8 * s) >> 2;         // first window quad
   const int chq = g.chf >> 2;
-  for (int c = grp; c < cu && !SM_ABL(2); c += G::K) {
-    const f32x4* b = l4 + c * chq;
-    const f32x4 a0 = b[f1q], a1 = b[f1q + 1];
-    const f32x4 w[6] = {b[f2q], b[f2q + 1], b[f2q + 2], b[f2q + 3], b[f2q + 4], b[f2q + 5]};
-    const f32x4 wl[5] = {w[0], w[1], w[2], w[3], w[4]};
-    const f32x4 wh[5] = {w[1], w[2], w[3], w[4], w[5]};
-    corr_fma_pairs_s2<G::D, 5>(lo, a0, wl);
-    corr_fma_pairs_s2<G::D, 5>(hi, a1, wh);
+  stage(0);
+  for (int chunk = 0; chunk < nchunk; ++chunk) {
+    __syncthreads();  // chunk is in LDS; the other buffer is free (chunk-1 consumed)
+    if (chunk + 1 < nchunk) stage(chunk + 1);
+    const int ce = min(cu - chunk * chk, chk);
+    const f32x4* bb = l4 + (chunk & 1) * chk * chq;
+    for (int c = grp; c < ce && !SM_ABL(2); c += G::K) {
+      const f32x4* b = bb + c * chq;
+      const f32x4 a0 = b[f1q], a1 = b[f1q + 1];
+      const f32x4 w[6] = {b[f2q], b[f2q + 1], b[f2q + 2], b[f2q + 3], b[f2q + 4], b[f2q + 5]};
+      const f32x4 wl[5] = {w[0], w[1], w[2], w[3], w[4]};
+      const f32x4 wh[5] = {w[1], w[2], w[3], w[4], w[5]};
+      corr_fma_pairs_s2<G::D, 5>(lo, a0, wl);
+      corr_fma_pairs_s2<G::D, 5>(hi, a1, wh);
+    }
   }
 
   // ---- K partial sums meet in LDS ([v][group][item]); group grp finalises v == grp mod K ----
@@ -195,7 +211,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_small(
     }
   }
   __syncthreads();  // every wave has read its partials: the LDS becomes the output block
-  const int hpp = (Ho - p + 1) / 2;  // parity rows that exist
+  // (hpp: parity rows that exist, above)
   float* blk = lds;                  // [oc][r][x], Wo floats per row
   if (valid && r < hpp) {
 #pragma unroll
@@ -289,7 +305,18 @@ static hipError_t launch_small(const void* in1, const void* in2, void* out, int 
   if (nsplit < 1) nsplit = 1;
   const int cps = (C + nsplit - 1) / nsplit;
   nsplit = (C + cps - 1) / cps;
-  const size_t data = ((size_t)cps * g.chf + 4) * 4;  // + scratch float
+  // two chunk buffers within the LDS (the K-group reduction reuses it afterwards)
+  int chk = (int)(163840 / (2 * 4 * (size_t)g.chf));
+  if (chk > cps) chk = cps;
+  {  // register staging: at most 32 passes of 512 / E channels per chunk
+    const int E = 2 * ((Ho + 1) / 2) * W;
+    const int cpt = E > 0 ? G::THREADS / E : 0;
+    if (cpt < 1) return hipErrorNotSupported;
+    if (chk > 32 * cpt) chk = 32 * cpt;
+  }
+  if (off != 0) return hipErrorNotSupported;
+  if (chk < 1) return hipErrorNotSupported;
+  const size_t data = (size_t)2 * chk * g.chf * 4;
   const size_t lds = data > (size_t)G::RED_BYTES ? data : (size_t)G::RED_BYTES;
   if (lds > 163840) return hipErrorNotSupported;
   if (nsplit > 1 && !partial) return hipErrorNotSupported;
@@ -309,7 +336,7 @@ static hipError_t launch_small(const void* in1, const void* in2, void* out, int 
   hipExtLaunchKernelGGL((corr_fwd_small<G>), dim3((unsigned)(2 * B), (unsigned)nsplit),
                         dim3(G::THREADS), lds, stream, ev0, ev1, 0, (const float*)in1,
                         (const float*)in2, (float*)out, (float*)partial, B, C, H, W, Ho, Wo,
-                        off, layout, divisor, inv, cps, g);
+                        off, layout, divisor, inv, cps, chk, g);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nsplit == 1) return e;
   const size_t total = (size_t)B * 81 * Ho * Wo;
@@ -334,6 +361,9 @@ hipError_t corr_forward_small_f32(const void* in1, const void* in2, void* out, i
   const int items = 9 * hp * nseg;
   // channel slices: enough workgroups to spread the staging loads (~128), at least 8
   // channels per slice, within the workspace
+  // channel slices: enough workgroups to spread the staging (~128), at least 8 channels per
+  // slice, within the workspace (measured at l0 / l1, B = 8: 8 slices + reduce beat one
+  // workgroup per parity half with every channel streamed through LDS, 10 vs 15 us at l0)
   int nsplit = 1;
   if (partial && max_splits > 1) {
     nsplit = (128 + 2 * B - 1) / (2 * B);
