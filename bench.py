@@ -125,7 +125,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_l4corr_pmc.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01d_l4corr_pmc.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -354,7 +354,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
       q *= inv_divisor;
     else
       q /= divisor;
-    *reinterpret_cast<f32x4*>(obase + (size_t)oc * Ho * Wo + 4 * h) = q;
+    st_out4(obase + (size_t)oc * Ho * Wo + 4 * h, q);
   };
   if constexpr (G::K == 1) {
 #pragma unroll

@@ -346,14 +346,14 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
   for (int ti = 0; ti < G::D; ++ti) {
     const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
     float* orow = out + (((size_t)n * OC + oc) * Ho + oy) * Wo;
-    float4 v;
+    st_f32x4 v;
     if (pow2)
-      v = make_float4(acc[ti][0] * inv_divisor, acc[ti][1] * inv_divisor,
-                      acc[ti][2] * inv_divisor, acc[ti][3] * inv_divisor);
+      v = st_f32x4{acc[ti][0] * inv_divisor, acc[ti][1] * inv_divisor,
+                   acc[ti][2] * inv_divisor, acc[ti][3] * inv_divisor};
     else
-      v = make_float4(acc[ti][0] / divisor, acc[ti][1] / divisor, acc[ti][2] / divisor,
-                      acc[ti][3] / divisor);
-    *reinterpret_cast<float4*>(orow + ox) = v;
+      v = st_f32x4{acc[ti][0] / divisor, acc[ti][1] / divisor, acc[ti][2] / divisor,
+                   acc[ti][3] / divisor};
+    st_out4(orow + ox, v);
   }
 }
 

@@ -251,7 +251,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_small(
   const int step_oc = (8 * rpi) / hpp, step_rr = (8 * rpi) - step_oc * hpp;
   for (int row = wv * rpi + sub; row < nrows + 8 * rpi; row += 8 * rpi) {
     if (row < nrows && x < Wo)
-      base[((size_t)oc * pstr + ystr * rr + yoff) * Wo + x] = blk[(oc * g.hp + rr) * Wo + x];
+      st_out1(base + ((size_t)oc * pstr + ystr * rr + yoff) * Wo + x, blk[(oc * g.hp + rr) * Wo + x]);
     oc += step_oc;
     rr += step_rr;
     if (rr >= hpp) {
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void sm_reduce(const float* __restrict__ parti
 #pragma unroll
     for (int k = 1; k < 16; ++k)
       if (k < nsplit) sum += v[k];
-    out[i] = inv_divisor != 0.f ? sum * inv_divisor : sum / divisor;
+    st_out1(out + i, inv_divisor != 0.f ? sum * inv_divisor : sum / divisor);
   }
 }
 

@@ -85,6 +85,33 @@ __device__ __forceinline__ void corr_fma_pairs_s2(float (&acc)[D][4], const pk_f
   }
 }
 
+// Output stores of the big result volumes.  PWC_STORE_POLICY (build-time, for measurement):
+// 0 = plain, 1 = nontemporal (nt, default: the l4 correlation 19.1 -> 17.1 us at an unchanged
+// bench step), 2 = write-through (sc1: the line is not kept dirty in the
+// XCD's L2, so the kernel boundary has less to write back).
+#ifndef PWC_STORE_POLICY
+#define PWC_STORE_POLICY 1
+#endif
+typedef float st_f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_out4(float* p, st_f32x4 v) {
+#if PWC_STORE_POLICY == 1
+  __builtin_nontemporal_store(v, reinterpret_cast<st_f32x4*>(p));
+#elif PWC_STORE_POLICY == 2
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#else
+  *reinterpret_cast<st_f32x4*>(p) = v;
+#endif
+}
+__device__ __forceinline__ void st_out1(float* p, float v) {
+#if PWC_STORE_POLICY == 1
+  __builtin_nontemporal_store(v, p);
+#elif PWC_STORE_POLICY == 2
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#else
+  *p = v;
+#endif
+}
+
 // XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle must
 // be bijective"): consecutive logical tiles land on the same XCD (and L2), so neighbouring
 // tiles that re-read each other's halo rows hit the same L2.  Pure speed choice.

@@ -208,7 +208,13 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
       acc = fmaf(masked(cur.r[i][1], m01), w01, acc);
       acc = fmaf(masked(cur.r[i][2], m10), w10, acc);
       acc = fmaf(masked(cur.r[i][3], m11), w11, acc);
-      if (c0 + i < C) out[((unsigned)(n * C + c0 + i)) * plane + pix] = from_f32<T>(acc);
+      if (c0 + i < C) {
+        T* o = out + ((unsigned)(n * C + c0 + i)) * plane + pix;
+        if constexpr (sizeof(T) == 4)
+          st_out1(reinterpret_cast<float*>(o), acc);
+        else
+          *o = from_f32<T>(acc);
+      }
     }
   }
 }
