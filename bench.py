@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--fused-levels", default=os.environ.get("PWC_BENCH_FUSED", "0,1"),
+                    help="levels run as one fused warp->correlation launch (WarpCorrelation)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01d_l4corr_pmc.json"))
     args = ap.parse_args()
 
@@ -138,7 +140,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from pwcnet_amd import _lib
-    from pwcnet_amd.ops import warp_forward, corr_forward
+    from pwcnet_amd.ops import warp_forward, corr_forward, warp_corr_forward
     from pwcnet_amd.shard import max_over_ranks
     lib = _lib.load()
 
@@ -166,11 +168,18 @@ def main():
         if ret != 1:
             _lib.check(ret, "bench corr_l4")
 
+    fused = {int(v) for v in args.fused_levels.split(",") if v.strip()}
+
     def pre(s):
-        """levels l0..l3 (warp + corr) and the l4 warp; returns the l4 warped features."""
-        for lv in s[:-1]:
-            w = warp_forward(lv["x2"], lv["flow"])
-            lv["corr"] = corr_forward(lv["x1"], w, **CORR_ARGS)
+        """levels l0..l3 (warp + corr; fused levels as one WarpCorrelation launch that also
+        emits x2_warp) and the l4 warp; returns the l4 warped features."""
+        for l, lv in enumerate(s[:-1]):
+            if l in fused:
+                lv["corr"], lv["x2w"] = warp_corr_forward(lv["x1"], lv["x2"], lv["flow"],
+                                                          **CORR_ARGS)
+            else:
+                lv["x2w"] = warp_forward(lv["x2"], lv["flow"])
+                lv["corr"] = corr_forward(lv["x1"], lv["x2w"], **CORR_ARGS)
         return warp_forward(s[-1]["x2"], s[-1]["flow"])
 
     # warm the kernels (first-call attribute setup) before any capture
@@ -258,6 +267,7 @@ def main():
             "levels": [list(s) for s in shapes],
             "parallelism": f"dp{world} (batch-sharded replicas, no data-path collective)",
             "buffer_sets": nsets,
+            "fused_levels": sorted(fused),
             "graph": bool(graphs),
         },
         "roofline": {

@@ -27,6 +27,8 @@
  *   pwc_warp_forward/backward <- WarpingLayer.forward (modules.py:31-42) + get_grid
  *                             (utils.py:3-8) + F.grid_sample/grid_sampler_2d_backward with
  *                             torch-0.4 semantics (bilinear, zeros, align_corners=True).
+ *   pwc_warp_corr_forward  <- the two calls of one pyramid level, model.py:80 (warp) + :83
+ *                             (corr), as one entry point (fused kernel where it applies).
  */
 #ifndef PWC_HOTPATH_H
 #define PWC_HOTPATH_H
@@ -48,7 +50,8 @@ extern "C" {
 #define PWC_DTYPE_F16 1
 #define PWC_DTYPE_BF16 2
 
-/* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook). */
+/* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
+ * 4: fused warp -> correlation). */
 PWC_API int pwc_abi_version(void);
 
 /* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
@@ -115,6 +118,22 @@ PWC_API int pwc_warp_forward(const void* x, const void* flow, void* out, int B, 
 PWC_API int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, void* grad_x,
                       void* grad_flow, int B, int C, int H, int W, int dtype, void* stream);
 
+/* One pyramid level of model.py:80-83: x2_warp = WarpingLayer(x2, flow), then
+ * out = Correlation(in1, x2_warp) exactly as pwc_warp_forward followed by pwc_corr_forward
+ * (same values: x2_warp bit-identical, out within fp32 summation order).  x2_warp may be NULL
+ * (not needed by the caller); it is written otherwise.  For model.py:24's configuration in
+ * fp32 this is ONE kernel launch per level where the level fits (no warped-feature round trip
+ * through HBM); other configurations run the two kernels.  `workspace` must hold
+ * pwc_warp_corr_workspace_size(..., emit_warp = x2_warp != NULL) bytes; NULL is accepted when
+ * x2_warp is given (the fallback then runs without channel splitting). */
+PWC_API size_t pwc_warp_corr_workspace_size(int B, int C, int H, int W, int pad_size,
+                                    int kernel_size, int max_displacement, int stride1,
+                                    int stride2, int dtype, int emit_warp);
+PWC_API int pwc_warp_corr_forward(const void* in1, const void* x2, const void* flow, void* x2_warp,
+                          void* out, int B, int C, int H, int W, int pad_size,
+                          int kernel_size, int max_displacement, int stride1, int stride2,
+                          int corr_multiply, int dtype, void* workspace,
+                          size_t workspace_bytes, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,8 @@ template <typename T>
 hipError_t warp_forward_t(const void*, const void*, void*, int, int, int, int, hipStream_t);
 hipError_t warp_backward_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                              int, hipStream_t);
+hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void*, int, int, int,
+                              int, float, int, hipStream_t);
 }  // namespace pwc
 
 namespace pwc {
@@ -86,7 +88,7 @@ int force_generic() {
 
 extern "C" {
 
-int pwc_abi_version(void) { return 3; }
+int pwc_abi_version(void) { return 4; }
 
 int pwc_time_next_corr(void* start_event, void* stop_event) {
   if ((start_event == nullptr) != (stop_event == nullptr))
@@ -342,6 +344,86 @@ int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, voi
     return fail(fn, "null buffer");
   return check_launch(fn, pwc::warp_backward_f32(x, flow, grad_out, grad_x, grad_flow, B, C, H,
                                                  W, (hipStream_t)stream));
+}
+
+
+// ---- fused warp -> correlation (model.py:80-83 as one call) ----
+// The fused kernel covers model.py:24's configuration (pad == md in {8, 9}, k 1, s1 1, s2 2)
+// for fp32 wherever one band workgroup holds the level; everything else runs the warp kernel
+// then the correlation kernels (x2_warp, or the workspace's tail when x2_warp is NULL, holds
+// the warped features in between).
+static bool warp_corr_fusable(int pad, int k, int md, int s1, int s2, int dtype) {
+  return dtype == PWC_DTYPE_F32 && k == 1 && s1 == 1 && s2 == 2 && pad == md &&
+         (md == 8 || md == 9);
+}
+
+static int fused_disabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = std::getenv("PWC_FUSED");
+    v = (s && s[0] == '0') ? 1 : 0;
+  }
+  return v;
+}
+
+static size_t elem_size(int dtype) { return dtype == PWC_DTYPE_F32 ? 4 : 2; }
+
+size_t pwc_warp_corr_workspace_size(int B, int C, int H, int W, int pad_size, int kernel_size,
+                                    int max_displacement, int stride1, int stride2, int dtype,
+                                    int emit_warp) {
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W) || (dtype < 0 || dtype > 2) ||
+      !corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo) ||
+      Ho <= 0 || Wo <= 0)
+    return 0;
+  // the unfused fallback may run: split-channel partials + (without x2_warp) a warp buffer
+  size_t ws = (pwc::corr_workspace_bytes(B, OC, Ho, Wo) + 255) & ~(size_t)255;
+  if (!emit_warp) ws += (size_t)B * C * H * W * elem_size(dtype);
+  return ws;
+}
+
+int pwc_warp_corr_forward(const void* in1, const void* x2, const void* flow, void* x2_warp,
+                          void* out, int B, int C, int H, int W, int pad_size, int kernel_size,
+                          int max_displacement, int stride1, int stride2, int corr_multiply,
+                          int dtype, void* workspace, size_t workspace_bytes, void* stream) {
+  (void)corr_multiply;
+  const char* fn = "pwc_warp_corr_forward";
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (!corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo))
+    return fail(fn, "invalid correlation parameters");
+  if (Ho <= 0 || Wo <= 0) return fail(fn, "empty correlation output");
+  if (dtype < 0 || dtype > 2) return fail(fn, "unsupported dtype");
+  if ((size_t)B * C * H * W && (!in1 || !x2 || !flow || !out)) return fail(fn, "null buffer");
+  const size_t need = pwc_warp_corr_workspace_size(B, C, H, W, pad_size, kernel_size,
+                                                   max_displacement, stride1, stride2, dtype,
+                                                   x2_warp != nullptr);
+  hipStream_t s = (hipStream_t)stream;
+  if (!fused_disabled() && warp_corr_fusable(pad_size, kernel_size, max_displacement, stride1,
+                                             stride2, dtype)) {
+    const hipError_t e = pwc::warp_corr_band_f32(in1, x2, flow, x2_warp, out, B, C, H, W,
+                                                 (float)C, 1, s);
+    if (e != hipErrorNotSupported) return check_launch(fn, e);
+  }
+  // two launches: warp into x2_warp (or the workspace tail), then the correlation
+  void* warped = x2_warp;
+  void* corr_ws = workspace;
+  size_t corr_ws_bytes = workspace_bytes;
+  if (!warped) {
+    if (!workspace || workspace_bytes < need)
+      return fail(fn, "x2_warp is NULL and the workspace is smaller than "
+                      "pwc_warp_corr_workspace_size(..., emit_warp=0)");
+    const size_t split = (pwc::corr_workspace_bytes(B, OC, Ho, Wo) + 255) & ~(size_t)255;
+    warped = (char*)workspace + split;
+    corr_ws_bytes = split;
+    if (split == 0) corr_ws = nullptr;
+  }
+  if (!pwc_warp_forward(x2, flow, warped, B, C, H, W, dtype, stream)) return 0;
+  return corr_forward_impl(fn, in1, warped, out, B, C, H, W, pad_size, kernel_size,
+                           max_displacement, stride1, stride2, dtype, corr_ws, corr_ws_bytes,
+                           stream);
 }
 
 }  // extern "C"

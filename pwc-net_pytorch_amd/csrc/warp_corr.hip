@@ -1,0 +1,491 @@
+// warp_corr.hip — one pyramid level of PWC-Net's hot path in ONE launch: the flow warp of the
+// second image's features followed by the correlation against the first (model.py:80-83):
+//   x2_warp = WarpingLayer(x2, flow)                     (modules.py:31-42, utils.py:3-8)
+//   out     = Correlation(pad 9, k 1, md 9, s1 1, s2 2)(x1, x2_warp)   (model.py:24;
+//             correlation_cuda_kernel.cu:34-106)
+// out[n, tj*9+ti, y, x] = sum_c x1[n,c,y,x] * x2_warp[n,c,y+2tj-8,x+2ti-8] / C, zeros outside.
+// x2_warp (returned by the reference Net in summaries['x2_warps'], model.py:107,113) is
+// optionally written too, bit-identical to warp.hip's.  WARP = false correlates x2 directly.
+//
+// Decomposition (coarse levels: a few hundred to a few thousand pixels per image, 96-192
+// channels).  An output row only meets f2 rows of its own parity and an output column only f2
+// columns of its own parity (2tj, 2ti are even), so one workgroup takes
+//   one image n  x  one row parity p  x  one band of R parity rows  x  T displacement rows tj
+// with EVERY channel staged in LDS at once (one batch of loads, no channel ring, no partial
+// volumes in HBM and no second launch): f1 = the band's R rows, f2 = the R + T - 1 parity rows
+// the band meets at those tj, full width.  In LDS each row is split into its even and odd
+// columns (parity-column space, where the displacement step 2ti becomes 1) with 4 zero slots
+// on each side of the f2 rows -- the reference's zero padding, and the warp's "zeros" mode for
+// rows outside the image -- so the inner loop has no bounds checks.  The warped f2 values are
+// computed while staging (bilinear gathers from x2 on the reference's fp32 coordinate chain,
+// warp_sample.cuh); the workgroup whose tj range holds tj = 4 (dy = 0) stages exactly its
+// band's rows and writes them to x2_warp, so every x2_warp element is written once.
+// Compute: item = (tj, row, column parity, 4-pixel segment), G channel groups per workgroup;
+// per channel one item reads 1 f1 quad + 3 f2 quads for 36 FMAs.  The G partial sums meet in
+// LDS in a fixed order (deterministic) and the result is written row by row (lane = x).
+#include <hip/hip_ext.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "warp_sample.cuh"
+
+namespace pwc {
+
+void take_launch_events(hipEvent_t* start, hipEvent_t* stop);  // capi.hip
+
+namespace band {
+
+constexpr int NT = 512;   // threads per workgroup (8 waves, 2 per SIMD)
+constexpr int D = 9;      // displacements per axis (md / s2 = 4)
+constexpr int MAXJ = 32;  // channels per staging batch per thread (loads in flight)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+struct Geo {
+  int Wq4;    // parity-column slots of an f1 row half (ceil(W/2) rounded up to 4)
+  int Wf;     // slots of an f2 row half: Wq4 + 8 (4 zero slots each side)
+  int S;      // 4-pixel segments per row half
+  int I;      // compute items: T * R * 2 * S
+  int G;      // channel groups (G * I <= NT)
+  int nb;     // bands per parity half
+  int units;  // B * 2 * nb
+  int f1f;    // floats of the f1 image: C * R * 2 * Wq4
+  int clr4;   // float4s of staging to clear
+  float inv_np1, inv_np2, inv_W, inv_I, inv_S;  // 1/d for qdiv
+  int abl;    // measurement only (PWC_BAND_ABL): 1 no f1 staging, 2 no f2 staging,
+              // 4 no FMA loop, 8 no epilogue, 16 no clear
+};
+
+// x / d for 0 <= x < 2^22 from a host-computed float 1/d: (x + 0.5) / d lies at least 0.5/d
+// from an integer and the float error is below that, so the truncation is exact (3 VALU
+// instead of a ~30-instruction integer division; issue slots bound these small kernels).
+__device__ __forceinline__ int qdiv(int x, float inv) {
+  return (int)(((float)x + 0.5f) * inv);
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global loads (__syncthreads() also drains vmcnt, which put a full memory round trip (~2 us
+// measured) in front of every barrier while the staging loads were in flight).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Phase timestamps (measurement only, PWC_BAND_ABL & 256): s_memrealtime (100 MHz) of
+// workgroup b's thread 0 at kernel entry and after each barrier -> g_band_dbg[b * 8 + k].
+__device__ unsigned long long g_band_dbg[4096 * 8];
+#define BAND_MARK(k)                                                                   \
+  do {                                                                                 \
+    if ((g.abl & 256) && threadIdx.x == 0 && blockIdx.x < 4096)                        \
+      g_band_dbg[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();             \
+  } while (0)
+
+template <int R, int T, bool WARP>
+__global__ __launch_bounds__(NT, 1) void warp_corr_band(
+    const float* __restrict__ f1, const float* __restrict__ x2, const float* __restrict__ flow,
+    float* __restrict__ x2w, float* __restrict__ out, int C, int H, int W, float divisor,
+    float inv_divisor, float halfx, float halfy, Geo g) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NR2 = R + T - 1;  // f2 parity rows staged
+  BAND_MARK(0);
+  const int t = threadIdx.x;
+  // blockIdx = tg * units + unit: the T-groups of one band are units apart (same XCD when
+  // units % 8 == 0), so they meet the same x1 / x2 rows in one L2 -- speed only
+  const int unit = blockIdx.x % g.units, tg = blockIdx.x / g.units;
+  const int b = unit % g.nb, np = unit / g.nb;
+  const int p = np & 1, n = np >> 1;
+  const int hp = (H - p + 1) >> 1;  // image rows of parity p
+  const int r0 = b * R, tj0 = tg * T;
+  const unsigned plane = (unsigned)(H * W);
+  float* f1s = lds;
+  float* f2s = lds + g.f1f;
+  const int ch1 = R * 2 * g.Wq4;     // f1 floats per channel
+  const int ch2 = NR2 * 2 * g.Wf;    // f2 floats per channel
+
+  // ---- staging.  f1 thread map: (band pixel, channel group); f2 thread map: (f2 pixel,
+  // channel group).  All global traffic is buffer loads/stores over image n of each tensor:
+  // the per-lane VGPR offset is fixed for the whole staging and the channel step is a scalar
+  // offset, so no per-load address arithmetic and no register reuse (re-writing a register an
+  // in-flight store still reads costs a vmcnt wait per store); offsets past the image -- the
+  // channels beyond C, idle lanes -- read 0 / drop the store in the buffer range check.  Every
+  // load of a thread is issued before anything waits: flow and f1 first, the LDS clear runs
+  // under them, then the bilinear gathers. ----
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t img_bytes = (uint32_t)C * plane * 4u;
+  const int np1 = R * W, ncg1 = NT / np1;
+  const int cg1 = qdiv(t, g.inv_np1), pix1 = t - cg1 * np1;
+  const int r1 = qdiv(pix1, g.inv_W), x1 = pix1 - r1 * W;
+  const bool ok1 = cg1 < ncg1 && r0 + r1 < hp && !(g.abl & 1);
+  const uint32_t vo1 =
+      ok1 ? ((uint32_t)cg1 * plane + (uint32_t)(2 * (r0 + r1) + p) * W + x1) * 4u : kOOB;
+  const int dst1 = (r1 * 2 + (x1 & 1)) * g.Wq4 + (x1 >> 1);
+
+  const int np2 = NR2 * W, ncg2 = NT / np2;
+  const int cg2 = qdiv(t, g.inv_np2), pix2 = t - cg2 * np2;
+  const int k2 = qdiv(pix2, g.inv_W), x2i = pix2 - k2 * W;
+  const int rr = r0 + tj0 - 4 + k2;  // parity row of f2
+  const bool ok2 = cg2 < ncg2 && rr >= 0 && rr < hp && !(g.abl & 2);
+  const int y2 = 2 * rr + p;
+  const unsigned src2 = (unsigned)(ok2 ? y2 : 0) * W + x2i;
+  const int dst2 = (k2 * 2 + (x2i & 1)) * g.Wf + (x2i >> 1) + 4;
+  // the dy = 0 workgroup of the band writes x2_warp (each element once in the grid)
+  const bool emit = WARP && ok2 && x2w != nullptr && tj0 <= 4 && 4 < tj0 + T &&
+                    k2 >= 4 - tj0 && k2 < 4 - tj0 + R;
+  const uint32_t cbase2 = (uint32_t)cg2 * plane;
+  const uint32_t vow = emit ? (cbase2 + src2) * 4u : kOOB;
+  const size_t img = (size_t)n * C * plane;
+  const __amdgpu_buffer_rsrc_t rs1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(f1 + img), (short)0, (int)img_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(x2 + img), (short)0, (int)img_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(x2w ? x2w + img : x2w), (short)0, x2w ? (int)img_bytes : 0, 0x00020000);
+  const uint32_t cs1 = (uint32_t)ncg1 * plane * 4u;  // bytes between a thread's channels
+  const uint32_t cs2 = (uint32_t)ncg2 * plane * 4u;
+
+  float fu = 0.f, fv = 0.f;
+  if constexpr (WARP) {
+    fu = flow[(unsigned)(2 * n + 0) * plane + src2];
+    fv = flow[(unsigned)(2 * n + 1) * plane + src2];
+  }
+  // channels per thread (uniform): iterations past it are skipped by a scalar branch
+  const int nj1 = (C + ncg1 - 1) / ncg1, nj2 = (C + ncg2 - 1) / ncg2;
+  int jb1 = 0, jb2 = 0;  // channel slot of the batch's first j
+  float v1[MAXJ];
+  auto f1_issue = [&]() {
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      if (jb1 + j >= nj1) break;
+      v1[j] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(rs1, (int)vo1, (int)((jb1 + j) * cs1), 0));
+    }
+  };
+  auto f1_store = [&]() {
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      if (jb1 + j >= nj1) break;
+      const int c = cg1 + (jb1 + j) * ncg1;
+      if (ok1 && c < C) f1s[c * ch1 + dst1] = v1[j];
+    }
+  };
+  f1_issue();
+
+  {  // zeros: padding slots, rows outside the image, columns past W
+    f32x4* z = reinterpret_cast<f32x4*>(lds);
+    for (int i = t; i < ((g.abl & 16) ? 0 : g.clr4); i += NT) z[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  lds_barrier();
+  BAND_MARK(1);
+
+  // bilinear setup of this thread's f2 pixel (warp.hip's chain, bit-identical samples)
+  Pairs kp{};
+  float w00 = 0.f, w01 = 0.f, w10 = 0.f, w11 = 0.f;
+  if (WARP) {
+    const float ix = src_coord(fu, x2i, W, halfx);
+    const float iy = src_coord(fv, y2, H, halfy);
+    const Bilinear bl = bilinear(ix, iy, H, W);
+    w00 = bl.wx0 * bl.wy0;
+    w01 = bl.wx1 * bl.wy0;
+    w10 = bl.wx0 * bl.wy1;
+    w11 = bl.wx1 * bl.wy1;
+    kp = pairs(bl, H, W);  // W >= 2 (launcher)
+  }
+  const uint32_t voA = ok2 ? (cbase2 + (WARP ? kp.i0 : src2)) * 4u : kOOB;
+  const uint32_t voB = ok2 ? (cbase2 + kp.i1) * 4u : kOOB;
+  float lo[MAXJ][2], hi[MAXJ][2];
+  auto f2_issue = [&]() {
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      if (jb2 + j >= nj2) break;
+      const int so = (int)((jb2 + j) * cs2);
+      if constexpr (WARP) {
+        const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(rs2, (int)voA, so, 0);
+        const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(rs2, (int)voB, so, 0);
+        lo[j][0] = __uint_as_float(a.x);
+        hi[j][0] = __uint_as_float(a.y);
+        lo[j][1] = __uint_as_float(b.x);
+        hi[j][1] = __uint_as_float(b.y);
+      } else {
+        lo[j][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs2, (int)voA, so, 0));
+      }
+    }
+  };
+  // blend + LDS write of every channel first; the x2_warp stores go out after the batch's last
+  // load was consumed (vmcnt retires in issue order: a store between loads delays them)
+  auto f2_store = [&]() {
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      if (jb2 + j >= nj2) break;
+      const int c = cg2 + (jb2 + j) * ncg2;
+      float val;
+      if constexpr (WARP) {
+        // warp.hip's blend, same operation order (bit-identical x2_warp)
+        const float c00 = kp.l_lo ? lo[j][0] : hi[j][0];
+        const float c01 = kp.r_lo ? lo[j][0] : hi[j][0];
+        const float c10 = kp.l_lo ? lo[j][1] : hi[j][1];
+        const float c11 = kp.r_lo ? lo[j][1] : hi[j][1];
+        float acc = 0.f;
+        acc = fmaf(masked(c00, kp.m00), w00, acc);
+        acc = fmaf(masked(c01, kp.m01), w01, acc);
+        acc = fmaf(masked(c10, kp.m10), w10, acc);
+        acc = fmaf(masked(c11, kp.m11), w11, acc);
+        val = acc;
+        lo[j][0] = acc;
+      } else {
+        val = lo[j][0];
+      }
+      if (ok2 && c < C) f2s[c * ch2 + dst2] = val;
+    }
+    if constexpr (WARP) {
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) {
+        if (jb2 + j >= nj2) break;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lo[j][0]), rsw, (int)vow,
+                                              (int)((jb2 + j) * cs2), 2 /* nt */);
+      }
+    }
+  };
+  f2_issue();
+  f1_store();
+  f2_store();
+  // further batches when a thread has more than MAXJ channels (uniform trip count)
+  const int nbat1 = (nj1 + MAXJ - 1) / MAXJ;
+  const int nbat2 = (nj2 + MAXJ - 1) / MAXJ;
+  for (int b = 1; b < max(nbat1, nbat2); ++b) {
+    jb1 = b * MAXJ;
+    jb2 = b * MAXJ;
+    const bool m1 = b < nbat1, m2 = b < nbat2;
+    if (m1) f1_issue();
+    if (m2) f2_issue();
+    if (m1) f1_store();
+    if (m2) f2_store();
+  }
+  lds_barrier();
+  BAND_MARK(2);
+
+  // ---- correlation: item (tt, r, q, s) of channel group grp ----
+  const int grp = qdiv(t, g.inv_I), it = t - grp * g.I;
+  float acc[D][4];
+#pragma unroll
+  for (int ti = 0; ti < D; ++ti)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc[ti][kk] = 0.f;
+  if (grp < g.G && !(g.abl & 4)) {
+    int rest = qdiv(it, g.inv_S);
+    const int s = it - rest * g.S;
+    const int q = rest & 1;
+    rest >>= 1;
+    const int r = rest % R, tt = rest / R;
+    const f32x4* pa = reinterpret_cast<const f32x4*>(f1s + (r * 2 + q) * g.Wq4 + 4 * s);
+    const f32x4* pb = reinterpret_cast<const f32x4*>(f2s + ((r + tt) * 2 + q) * g.Wf + 4 * s);
+    const int s1 = ch1 >> 2, s2 = ch2 >> 2;
+    // one channel's quads in flight while the previous channel's 36 FMAs issue
+    int c = grp;
+    f32x4 a = pa[c * s1], q0 = pb[c * s2], q1 = pb[c * s2 + 1], q2 = pb[c * s2 + 2];
+    for (; c < C; c += g.G) {
+      const int cn = c + g.G < C ? c + g.G : c;
+      const f32x4 an = pa[cn * s1], n0 = pb[cn * s2], n1 = pb[cn * s2 + 1],
+                  n2 = pb[cn * s2 + 2];
+      const float w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                           q2.x, q2.y, q2.z, q2.w};
+      const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int ti = 0; ti < D; ++ti)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) acc[ti][kk] = fmaf(av[kk], w[kk + ti], acc[ti][kk]);
+      a = an;
+      q0 = n0;
+      q1 = n1;
+      q2 = n2;
+    }
+  }
+  lds_barrier();  // staging dead: the partial sums reuse it
+  BAND_MARK(3);
+  if (grp < g.G) {
+    f32x4* rp = reinterpret_cast<f32x4*>(lds) + (grp * g.I + it) * D;
+#pragma unroll
+    for (int ti = 0; ti < D; ++ti)
+      rp[ti] = f32x4{acc[ti][0], acc[ti][1], acc[ti][2], acc[ti][3]};
+  }
+  lds_barrier();
+  BAND_MARK(4);
+
+  // ---- epilogue: fixed-order sum of the G groups, / divisor (cu:100), rows of W (lane = x) --
+  const int nout = (g.abl & 8) ? 0 : T * D * R * W;
+  for (int o = t; o < nout; o += NT) {
+    int rest = qdiv(o, g.inv_W);
+    const int x = o - rest * W;
+    const int r = rest % R;
+    rest /= R;
+    const int ti = rest % D, tt = rest / D;
+    const int tj = tj0 + tt, row = r0 + r;
+    if (tj >= D || row >= hp) continue;
+    const int i = x >> 1;
+    const int it2 = ((tt * R + r) * 2 + (x & 1)) * g.S + (i >> 2);
+    const float* sp = lds + (it2 * D + ti) * 4 + (i & 3);
+    const int gstride = g.I * D * 4;
+    // fixed order: four interleaved partial sums (independent LDS reads in flight)
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int gg = 0;
+    for (; gg + 4 <= g.G; gg += 4) {
+      s0 += sp[gg * gstride];
+      s1 += sp[(gg + 1) * gstride];
+      s2 += sp[(gg + 2) * gstride];
+      s3 += sp[(gg + 3) * gstride];
+    }
+    for (; gg < g.G; ++gg) s0 += sp[gg * gstride];
+    float sum = (s0 + s1) + (s2 + s3);
+    sum = inv_divisor != 0.f ? sum * inv_divisor : sum / divisor;
+    st_out1(out + ((unsigned)(n * (D * D) + tj * D + ti) * H + (2 * row + p)) * W + x, sum);
+  }
+  if (g.abl & 256) {
+    __syncthreads();
+    BAND_MARK(5);
+  }
+}
+
+struct Cfg {
+  int R, T;
+};
+
+// PWC_BAND_CFG="R,T[,G]" overrides the per-level choice (measurement).
+static bool env_cfg(int* R, int* T, int* G) {
+  const char* e = std::getenv("PWC_BAND_CFG");
+  if (!e || !*e) return false;
+  int r = 0, tt = 0, gg = 0;
+  const int k = std::sscanf(e, "%d,%d,%d", &r, &tt, &gg);
+  if (k < 2) return false;
+  *R = r;
+  *T = tt;
+  if (k == 3) *G = gg;
+  return true;
+}
+
+template <int R, int T, bool WARP>
+static hipError_t launch(const float* f1, const float* x2, const float* flow, float* x2w,
+                         float* out, int B, int C, int H, int W, float divisor, float inv,
+                         float halfx, float halfy, Geo g, size_t lds, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&warp_corr_band<R, T, WARP>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int ntg = (D + T - 1) / T;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  take_launch_events(&ev0, &ev1);
+  hipExtLaunchKernelGGL((warp_corr_band<R, T, WARP>), dim3((unsigned)(g.units * ntg)), dim3(NT),
+                        lds, stream, ev0, ev1, 0, f1, x2, flow, x2w, out, C, H, W, divisor, inv,
+                        halfx, halfy, g);
+  return hipGetLastError();
+}
+
+// Geometry for (R, T); false if it does not fit one workgroup.
+static bool make_geo(int B, int C, int H, int W, int R, int T, int Greq, Geo* g, size_t* lds) {
+  const int Wq = (W + 1) / 2;
+  g->Wq4 = (Wq + 3) & ~3;
+  g->Wf = g->Wq4 + 8;
+  g->S = g->Wq4 / 4;
+  g->I = T * R * 2 * g->S;
+  if (g->I > NT || R * W > NT || (R + T - 1) * W > NT) return false;
+  int G = NT / g->I;
+  // channel groups: at least 4 channels per group and at most 32 groups (the epilogue sums G
+  // partials per output)
+  int gc = C / 4;
+  if (gc > 32) gc = 32;
+  if (gc < 1) gc = 1;
+  if (G > gc) G = gc;
+  if (Greq > 0 && Greq <= NT / g->I) G = Greq;
+  g->G = G;
+  const int hp = (H + 1) / 2;
+  g->nb = (hp + R - 1) / R;
+  g->units = B * 2 * g->nb;
+  g->f1f = C * R * 2 * g->Wq4;
+  const size_t stage = (size_t)(g->f1f + C * (R + T - 1) * 2 * g->Wf) * 4;
+  const size_t red = (size_t)G * g->I * D * 16;
+  g->clr4 = (int)(stage / 16);
+  g->inv_np1 = 1.f / (float)(R * W);
+  g->inv_np2 = 1.f / (float)((R + T - 1) * W);
+  g->inv_W = 1.f / (float)W;
+  g->inv_I = 1.f / (float)g->I;
+  g->inv_S = 1.f / (float)g->S;
+  const char* ab = std::getenv("PWC_BAND_ABL");
+  g->abl = ab ? std::atoi(ab) : 0;
+  *lds = stage > red ? stage : red;
+  return *lds <= 160 * 1024;
+}
+
+}  // namespace band
+
+// measurement only: copy the phase timestamps of the last PWC_BAND_ABL & 256 launch
+extern "C" __attribute__((visibility("default"))) int pwc_debug_band_times(void* dst, int n) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(band::g_band_dbg),
+                             sizeof(unsigned long long) * (size_t)n) == hipSuccess;
+}
+
+extern "C" __attribute__((visibility("default"))) int pwc_debug_band_reset(void) {
+  static unsigned long long zeros[4096 * 8];
+  return hipMemcpyToSymbol(HIP_SYMBOL(band::g_band_dbg), zeros, sizeof(zeros)) == hipSuccess;
+}
+
+// Fused warp -> correlation for Correlation(pad == md in {8, 9}, k 1, s1 1, s2 2), fp32,
+// raster channel order.  hipErrorNotSupported when the level does not fit a band workgroup
+// (the caller then runs the warp and correlation kernels separately).  `warp` = 0 correlates
+// x2 directly (flow and x2w unused).
+hipError_t warp_corr_band_f32(const void* f1, const void* x2, const void* flow, void* x2w,
+                              void* out, int B, int C, int H, int W, float divisor, int warp,
+                              hipStream_t stream) {
+  using namespace band;
+  if (B == 0 || C == 0 || H == 0 || W == 0) return hipSuccess;
+  if (W < 2 || (size_t)B * C * H * W >= (1ull << 31) || (size_t)B * 81 * H * W >= (1ull << 31))
+    return hipErrorNotSupported;
+  // per-level choice: the whole parity half in one band where it fits, one tj per workgroup
+  int R = 0, T = 1, Greq = 0;
+  const int hp = (H + 1) / 2;
+  if (!env_cfg(&R, &T, &Greq)) {  // measured at 384x448, B = 8 (tools/kbench.py)
+    if (hp <= 3) {
+      R = 3;  // l0: 7.7 us (warp 3.1 + correlation 10.9 unfused)
+      T = 1;
+    } else if (hp <= 6) {
+      R = 2;  // l1: 10.7 us (3.4 + 13.4 unfused)
+      T = 3;
+    } else {
+      R = 3;  // l2 and larger (the bench keeps l2..l4 unfused: 17.7 vs 3.6 + 11.4 us at l2)
+      T = 3;
+    }
+  }
+  Geo g;
+  size_t lds;
+  if (!make_geo(B, C, H, W, R, T, Greq, &g, &lds)) return hipErrorNotSupported;
+  const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
+  int ex;
+  const float m = std::frexp(divisor, &ex);
+  const float inv = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
+  const float* a = (const float*)f1;
+  const float* b = (const float*)x2;
+  const float* fl = (const float*)flow;
+  float* w = (float*)x2w;
+  float* o = (float*)out;
+#define PWC_BAND(RR, TT)                                                                     \
+  if (R == RR && T == TT)                                                                    \
+    return warp ? launch<RR, TT, true>(a, b, fl, w, o, B, C, H, W, divisor, inv, halfx, halfy, \
+                                       g, lds, stream)                                       \
+                : launch<RR, TT, false>(a, b, fl, w, o, B, C, H, W, divisor, inv, halfx,       \
+                                        halfy, g, lds, stream);
+  PWC_BAND(3, 1)
+  PWC_BAND(6, 1)
+  PWC_BAND(4, 1)
+  PWC_BAND(2, 1)
+  PWC_BAND(2, 3)
+  PWC_BAND(4, 3)
+  PWC_BAND(3, 3)
+  PWC_BAND(6, 3)
+#undef PWC_BAND
+  return hipErrorNotSupported;
+}
+
+}  // namespace pwc

@@ -43,8 +43,10 @@ SYMBOLS = {
     "pwc_cost_volume_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 6 + [_P]),
     "pwc_warp_forward": (_I, [_P, _P, _P] + [_I] * 5 + [_P]),
     "pwc_warp_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 5 + [_P]),
+    "pwc_warp_corr_workspace_size": (_Z, [_I] * 11),
+    "pwc_warp_corr_forward": (_I, [_P] * 5 + [_I] * 11 + [_P, _Z, _P]),
 }
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lock = threading.Lock()
 _lib = None

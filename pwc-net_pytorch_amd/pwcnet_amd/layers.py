@@ -3,6 +3,7 @@
 * ``Correlation``     — correlation_package/modules/correlation.py:6-27 (same ctor, no params)
 * ``WarpingLayer``    — modules.py:25-42 (ctor takes the reference's ``args`` namespace)
 * ``CostVolumeLayer`` — modules.py:45-74 (ctor reads ``args.search_range``)
+* ``WarpCorrelation`` — model.py:80-83 (warp, then correlation) as one module / one launch
 * ``get_grid``        — utils.py:3-8 (host-built normalised base grid, for API completeness;
   the HIP warp recomputes it in registers and never calls this)
 """
@@ -11,7 +12,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .ops import CorrelationFunction, CostVolumeFunction, WarpFunction
+from .ops import CorrelationFunction, CostVolumeFunction, WarpCorrelationFunction, WarpFunction
 
 
 class Correlation(nn.Module):
@@ -57,6 +58,34 @@ class WarpingLayer(nn.Module):
 
     def forward(self, x, flow):
         return WarpFunction.apply(x, flow)
+
+
+class WarpCorrelation(nn.Module):
+    """One pyramid level of model.py:80-83 in one call:
+
+        x2_warp = self.warping_layer(x2, flow)      # model.py:80
+        corr = self.corr(x1, x2_warp)               # model.py:83
+    becomes
+        corr, x2_warp = self.warp_corr(x1, x2, flow)
+
+    Same ctor as ``Correlation`` (model.py:24's values by default).  Values equal the two
+    reference layers applied in sequence; gradients flow to x1, x2 and flow.
+    """
+
+    def __init__(self, pad_size=9, kernel_size=1, max_displacement=9, stride1=1, stride2=2,
+                 corr_multiply=1):
+        super().__init__()
+        self.pad_size = pad_size
+        self.kernel_size = kernel_size
+        self.max_displacement = max_displacement
+        self.stride1 = stride1
+        self.stride2 = stride2
+        self.corr_multiply = corr_multiply
+
+    def forward(self, x1, x2, flow):
+        return WarpCorrelationFunction.apply(x1, x2, flow, self.pad_size, self.kernel_size,
+                                             self.max_displacement, self.stride1, self.stride2,
+                                             self.corr_multiply)
 
 
 class CostVolumeLayer(nn.Module):

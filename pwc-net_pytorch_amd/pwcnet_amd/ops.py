@@ -237,6 +237,70 @@ class WarpFunction(Function):
         return gx, gf
 
 
+# ---------------------------------------------------------------------------------------
+# one pyramid level of model.py:80-83: warp then correlation, fused
+# ---------------------------------------------------------------------------------------
+def warp_corr_forward(input1, x2, flow, pad_size, kernel_size, max_displacement, stride1,
+                      stride2, corr_multiply=1, emit_warp=True):
+    """(corr, x2_warp) = (Correlation(input1, WarpingLayer(x2, flow)), WarpingLayer(x2, flow)).
+
+    Same values as ``warp_forward`` followed by ``corr_forward`` (x2_warp bit-identical); for
+    model.py:24's configuration in fp32 the pair runs as one kernel launch per level.
+    ``emit_warp=False`` skips writing x2_warp (returned as None)."""
+    _check_inputs("WarpCorrelation", input1, x2, flow)
+    if input1.shape != x2.shape:
+        raise ValueError(f"WarpCorrelation: input shapes differ {tuple(input1.shape)} vs "
+                         f"{tuple(x2.shape)}")
+    B, C, H, W = input1.shape
+    if tuple(flow.shape) != (B, 2, H, W):
+        raise ValueError(f"WarpCorrelation: flow shape {tuple(flow.shape)} != {(B, 2, H, W)}")
+    _i32(B, C, H, W, input1.numel())
+    input1, x2, flow = input1.contiguous(), x2.contiguous(), flow.contiguous()
+    OC, Ho, Wo = _lib.corr_output_shape(H, W, pad_size, kernel_size, max_displacement, stride1,
+                                        stride2)
+    out = torch.empty((B, OC, Ho, Wo), dtype=input1.dtype, device=input1.device)
+    x2w = torch.empty_like(x2) if emit_warp else None
+    if out.numel() == 0:
+        return out, x2w
+    lib = _lib.load()
+    dt = _lib.DTYPE_CODES[input1.dtype]
+    nws = lib.pwc_warp_corr_workspace_size(B, C, H, W, pad_size, kernel_size, max_displacement,
+                                           stride1, stride2, dt, int(emit_warp))
+    ws, wsp = _workspace(nws, input1.device)
+    _lib.check(lib.pwc_warp_corr_forward(
+        _ptr(input1), _ptr(x2), _ptr(flow), _ptr(x2w) if emit_warp else ctypes.c_void_p(0),
+        _ptr(out), B, C, H, W, pad_size, kernel_size, max_displacement, stride1, stride2,
+        corr_multiply, dt, wsp, nws, _stream(input1.device)), "WarpCorrelation_forward")
+    del ws
+    return out, x2w
+
+
+class WarpCorrelationFunction(Function):
+    """autograd for model.py:80-83 as one op: outputs (corr, x2_warp).  Backward chains the
+    reference's two backward passes: correlation (cu:108-290) into the warped features, plus
+    any gradient arriving on x2_warp itself, then grid_sample's (warp_backward)."""
+
+    @staticmethod
+    def forward(ctx, input1, x2, flow, pad_size=9, kernel_size=1, max_displacement=9,
+                stride1=1, stride2=2, corr_multiply=1):
+        with torch.cuda.device(input1.device) if input1.is_cuda else _nullctx():
+            out, x2w = warp_corr_forward(input1, x2, flow, pad_size, kernel_size,
+                                         max_displacement, stride1, stride2, corr_multiply)
+        ctx.save_for_backward(input1, x2.contiguous(), flow.contiguous(), x2w)
+        ctx.args = (pad_size, kernel_size, max_displacement, stride1, stride2, corr_multiply)
+        return out, x2w
+
+    @staticmethod
+    def backward(ctx, grad_corr, grad_x2w):
+        input1, x2, flow, x2w = ctx.saved_tensors
+        with torch.cuda.device(input1.device):
+            # unused outputs arrive as zeros (autograd materialises them)
+            g1, gw = corr_backward(input1, x2w, grad_corr, *ctx.args)
+            gw = gw + grad_x2w
+            gx2, gflow = warp_backward(x2, flow, gw)
+        return (g1, gx2, gflow) + (None,) * 6
+
+
 class _nullctx:
     def __enter__(self):
         return self

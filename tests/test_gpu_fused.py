@@ -1,0 +1,177 @@
+"""GPU parity of the fused warp -> correlation path (model.py:80-83 as one call,
+``pwc_warp_corr_forward`` / ``WarpCorrelation``) against the CPU oracle chain
+``oracle.warp_forward`` -> ``oracle.corr_forward`` (fp64) and against the unfused HIP kernels.
+
+Tolerances: corr 1e-5 abs + 1e-5 rel (BASELINE.json north_star), gradients 1e-4 (config 5);
+x2_warp must be BIT-identical to ``pwc_warp_forward`` (same sample chain, same blend order).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+# (B, C, H, W): the pyramid levels at 384x448 (model.py:72 order, l0..l4), ragged shapes
+LEVELS = [(2, 192, 6, 7), (2, 128, 12, 14), (2, 96, 24, 28), (1, 64, 48, 56), (1, 32, 96, 112)]
+RAGGED = [(1, 8, 5, 3), (2, 16, 7, 9), (1, 24, 13, 15), (1, 12, 2, 2), (1, 40, 11, 30),
+          (3, 3, 9, 4)]
+# band configurations (R parity rows, T displacement rows per workgroup[, channel groups])
+CFGS = ["", "2,1", "3,3", "4,3", "6,1,1", "2,3,5"]
+
+
+def _t(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def _inputs(seed, B, C, H, W, flow_sigma=2.0):
+    rng = np.random.default_rng(seed)
+    a = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    b = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    f = (rng.standard_normal((B, 2, H, W)) * flow_sigma).astype(np.float32)
+    return a, b, f
+
+
+@pytest.fixture
+def band_cfg(request):
+    old = os.environ.get("PWC_BAND_CFG")
+    os.environ["PWC_BAND_CFG"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("PWC_BAND_CFG", None)
+    else:
+        os.environ["PWC_BAND_CFG"] = old
+
+
+def _check(a, b, f, out, x2w, md=9):
+    wref = O.warp_forward(b, f)
+    cref = O.corr_forward(a, wref, md, 1, md, 1, 2)
+    np.testing.assert_allclose(_np(out), cref, rtol=1e-5, atol=1e-5)
+    if x2w is not None:
+        np.testing.assert_allclose(_np(x2w), wref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape", LEVELS + RAGGED, ids=lambda s: "B{}C{}_{}x{}".format(*s))
+@pytest.mark.parametrize("band_cfg", CFGS, indirect=True, ids=lambda c: "cfg" + (c or "auto"))
+def test_fused_vs_oracle(shape, band_cfg):
+    from pwcnet_amd.ops import warp_corr_forward, warp_forward
+    B, C, H, W = shape
+    a, b, f = _inputs(hash((shape, band_cfg)) % 2**32, *shape)
+    out, x2w = warp_corr_forward(_t(a), _t(b), _t(f), 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    _check(a, b, f, out, x2w)
+    # x2_warp bit-identical to the standalone warp kernel
+    ref_w = warp_forward(_t(b), _t(f))
+    assert torch.equal(x2w, ref_w)
+
+
+@pytest.mark.parametrize("shape", [(8, 192, 6, 7), (8, 128, 12, 14), (8, 96, 24, 28)],
+                         ids=lambda s: "B{}C{}_{}x{}".format(*s))
+def test_fused_full_batch_levels(shape):
+    """BASELINE config 2's batch (B=8) at the coarse levels, flows up to far out of the image."""
+    from pwcnet_amd.ops import warp_corr_forward
+    a, b, f = _inputs(11, *shape, flow_sigma=4.0)
+    out, x2w = warp_corr_forward(_t(a), _t(b), _t(f), 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    _check(a, b, f, out, x2w)
+
+
+def test_fused_matches_unfused_and_emit_flag():
+    from pwcnet_amd.ops import corr_forward, warp_corr_forward, warp_forward
+    a, b, f = _inputs(5, 2, 96, 24, 28)
+    out, x2w = warp_corr_forward(_t(a), _t(b), _t(f), 9, 1, 9, 1, 2)
+    out2, none = warp_corr_forward(_t(a), _t(b), _t(f), 9, 1, 9, 1, 2, emit_warp=False)
+    assert none is None
+    assert torch.equal(out, out2)  # same kernel, same order: bitwise
+    ref = corr_forward(_t(a), warp_forward(_t(b), _t(f)), 9, 1, 9, 1, 2)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_fused_deterministic():
+    from pwcnet_amd.ops import warp_corr_forward
+    a, b, f = _inputs(6, 4, 128, 12, 14)
+    o1, w1 = warp_corr_forward(_t(a), _t(b), _t(f), 9, 1, 9, 1, 2)
+    o2, w2 = warp_corr_forward(_t(a), _t(b), _t(f), 9, 1, 9, 1, 2)
+    assert torch.equal(o1, o2) and torch.equal(w1, w2)
+
+
+def test_fused_zero_flow_is_plain_correlation():
+    """model.py:75-76: level 0 runs with flow = 0, i.e. x2_warp == x2 (align_corners=True)."""
+    from pwcnet_amd.ops import corr_forward, warp_corr_forward
+    a, b, _ = _inputs(8, 2, 192, 6, 7)
+    f = np.zeros((2, 2, 6, 7), np.float32)
+    out, x2w = warp_corr_forward(_t(a), _t(b), _t(f), 9, 1, 9, 1, 2)
+    torch.testing.assert_close(x2w, _t(b), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(out, corr_forward(_t(a), _t(b), 9, 1, 9, 1, 2), rtol=1e-5,
+                               atol=1e-5)
+
+
+@pytest.mark.parametrize("md", [8, 9])
+def test_fused_md8(md):
+    from pwcnet_amd.ops import warp_corr_forward
+    a, b, f = _inputs(9, 2, 32, 12, 14)
+    out, x2w = warp_corr_forward(_t(a), _t(b), _t(f), md, 1, md, 1, 2)
+    torch.cuda.synchronize()
+    _check(a, b, f, out, x2w, md=md)
+
+
+@pytest.mark.parametrize("params", [(4, 1, 4, 1, 1), (9, 1, 9, 1, 2), (3, 3, 2, 1, 1)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_fused_fallback_configs(params, dtype):
+    """Configurations / dtypes the band kernel does not cover run warp + correlation; the
+    result equals the two ops called separately (bitwise: same kernels)."""
+    from pwcnet_amd.ops import corr_forward, warp_corr_forward, warp_forward
+    a, b, f = _inputs(10, 2, 16, 20, 24)
+    A, Bt, F = _t(a, dtype), _t(b, dtype), _t(f, dtype)
+    for emit in (True, False):
+        out, x2w = warp_corr_forward(A, Bt, F, *params, emit_warp=emit)
+        w = warp_forward(Bt, F)
+        ref = corr_forward(A, w, *params)
+        if dtype == torch.float32 and params == (9, 1, 9, 1, 2):
+            torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+        else:
+            assert torch.equal(out, ref)
+        if emit:
+            assert torch.equal(x2w, w)
+
+
+def test_fused_empty_batch():
+    from pwcnet_amd.ops import warp_corr_forward
+    x = torch.zeros(0, 8, 12, 14, device=DEV)
+    fl = torch.zeros(0, 2, 12, 14, device=DEV)
+    out, x2w = warp_corr_forward(x, x, fl, 9, 1, 9, 1, 2)
+    assert tuple(out.shape) == (0, 81, 12, 14) and tuple(x2w.shape) == (0, 8, 12, 14)
+
+
+def test_warp_correlation_module_autograd():
+    """WarpCorrelation (model.py:80-83 in one module): forward and gradients to x1, x2, flow
+    against the oracle chain (corr backward into the warped features, then warp backward),
+    with a gradient also arriving on x2_warp (as when summaries feed a loss)."""
+    import pwcnet_amd
+    a, b, f = _inputs(12, 2, 32, 12, 14)
+    x1 = _t(a).requires_grad_(True)
+    x2 = _t(b).requires_grad_(True)
+    fl = _t(f).requires_grad_(True)
+    layer = pwcnet_amd.WarpCorrelation(pad_size=9, kernel_size=1, max_displacement=9,
+                                       stride1=1, stride2=2, corr_multiply=1)
+    out, x2w = layer(x1, x2, fl)
+    rng = np.random.default_rng(13)
+    g = rng.standard_normal(out.shape).astype(np.float32)
+    gw_extra = rng.standard_normal(x2w.shape).astype(np.float32)
+    torch.autograd.backward([out, x2w], [_t(g), _t(gw_extra)])
+    wref = O.warp_forward(b, f)
+    np.testing.assert_allclose(_np(out), O.corr_forward(a, wref, 9, 1, 9, 1, 2), rtol=1e-5,
+                               atol=1e-5)
+    g1, gw = O.corr_backward(a, wref, g, 9, 1, 9, 1, 2)
+    gx2, gfl = O.warp_backward(b, f, gw + gw_extra)
+    np.testing.assert_allclose(_np(x1.grad), g1, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(x2.grad), gx2, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(fl.grad), gfl, rtol=1e-3, atol=1e-3)

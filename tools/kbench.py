@@ -18,24 +18,30 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from pwcnet_amd.ops import corr_backward, corr_forward, warp_backward, warp_forward  # noqa
+from pwcnet_amd.ops import (corr_backward, corr_forward, warp_backward, warp_corr_forward,  # noqa
+                            warp_forward)
 
 
 def timeit(fn, sets, iters):
-    """Mean device time per launch over `iters` back-to-back launches (rotating buffer sets)
-    between two events, repeated 5 times; returns (median-of-5, min-of-5) in microseconds.
-    Back-to-back launches keep the queue full, so host launch latency is not measured (the
-    ~1-2 us inter-kernel gap of the GPU is)."""
+    """Mean device time per launch over `iters` back-to-back launches (rotating buffer sets),
+    captured into one hipGraph and replayed between two events, 5 times; returns (median-of-5,
+    min-of-5) in microseconds.  The graph removes host launch cost (Python + ctypes + the
+    allocator), which otherwise exceeds the device time of the small levels; the GPU's own
+    inter-kernel gap stays in."""
     for s in sets:
         fn(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(iters):
+            fn(sets[i % len(sets)])
+    g.replay()
     torch.cuda.synchronize()
     res = []
     for _ in range(5):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda._sleep(2_000_000)  # let the host enqueue ahead of the device
         a.record()
-        for i in range(iters):
-            fn(sets[i % len(sets)])
+        g.replay()
         b.record()
         torch.cuda.synchronize()
         res.append(a.elapsed_time(b) * 1e3 / iters)
@@ -52,6 +58,9 @@ def main():
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--backward", action="store_true")
     ap.add_argument("--levels", default="0,1,2,3,4")
+    ap.add_argument("--ops", default="corr,warp,fused")
+    ap.add_argument("--tag", default="")
+    ap.add_argument("--sets", type=int, default=0, help="buffer sets (0 = past the MALL)")
     args = ap.parse_args()
     dt = torch.float32 if args.dtype == "fp32" else torch.float16
     esz = 4 if dt == torch.float32 else 2
@@ -63,22 +72,36 @@ def main():
         if l not in levels:
             continue
         per = (3 * C * h * w + 83 * h * w) * B * esz
-        n = max(2, int(2 * 256 * 2 ** 20 / per) + 1)
+        n = args.sets or max(2, int(2 * 256 * 2 ** 20 / per) + 1)
         g = torch.Generator(device=dev).manual_seed(l)
         sets = [dict(x1=torch.randn(B, C, h, w, device=dev, generator=g).to(dt),
                      x2=torch.randn(B, C, h, w, device=dev, generator=g).to(dt),
                      fl=(torch.randn(B, 2, h, w, device=dev, generator=g) * 2).to(dt))
                 for _ in range(n)]
-        med, mean = timeit(lambda s: corr_forward(s["x1"], s["x2"], 9, 1, 9, 1, 2), sets,
-                           args.iters)
+        ops = args.ops.split(",")
         cb = bench.corr_bytes_per_pair(C, h, w, esz) * B
-        print(json.dumps(dict(level=l, op="corr_fwd", path=path, shape=[B, C, h, w],
-                              us=round(med, 2), min_us=round(mean, 2),
-                              gbs=round(cb / (med * 1e-6) / 1e9, 1))))
-        med, mean = timeit(lambda s: warp_forward(s["x2"], s["fl"]), sets, args.iters)
+        if "corr" in ops:
+            med, mean = timeit(lambda s: corr_forward(s["x1"], s["x2"], 9, 1, 9, 1, 2), sets,
+                               args.iters)
+            print(json.dumps(dict(level=l, op="corr_fwd", path=path, shape=[B, C, h, w],
+                                  us=round(med, 2), min_us=round(mean, 2),
+                                  gbs=round(cb / (med * 1e-6) / 1e9, 1), tag=args.tag)))
         wb = (2 * C * h * w + 2 * h * w) * B * esz
-        print(json.dumps(dict(level=l, op="warp_fwd", shape=[B, C, h, w], us=round(med, 2),
-                              min_us=round(mean, 2), gbs=round(wb / (med * 1e-6) / 1e9, 1))))
+        if "warp" in ops:
+            med, mean = timeit(lambda s: warp_forward(s["x2"], s["fl"]), sets, args.iters)
+            print(json.dumps(dict(level=l, op="warp_fwd", shape=[B, C, h, w], us=round(med, 2),
+                                  min_us=round(mean, 2), gbs=round(wb / (med * 1e-6) / 1e9, 1),
+                                  tag=args.tag)))
+        if "fused" in ops:
+            # one level of model.py:80-83 (x2_warp emitted): bytes = read x1, x2, flow, write
+            # x2_warp and the volume
+            fb = (3 * C * h * w + 2 * h * w + 81 * h * w) * B * esz
+            med, mean = timeit(lambda s: warp_corr_forward(s["x1"], s["x2"], s["fl"], 9, 1, 9,
+                                                           1, 2), sets, args.iters)
+            print(json.dumps(dict(level=l, op="warp_corr", shape=[B, C, h, w],
+                                  band=os.environ.get("PWC_BAND_CFG", ""), us=round(med, 2),
+                                  min_us=round(mean, 2), gbs=round(fb / (med * 1e-6) / 1e9, 1),
+                                  tag=args.tag)))
         if args.backward and dt == torch.float32:
             go = torch.randn(B, 81, h, w, device=dev)
             med, mean = timeit(lambda s: corr_backward(s["x1"], s["x2"], go, 9, 1, 9, 1, 2),
