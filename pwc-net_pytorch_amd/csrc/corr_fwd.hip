@@ -501,6 +501,27 @@ static bool pt_disabled() {
   return v == 1;
 }
 
+// The band kernel of warp_corr.hip (without the warp) serves model.py:24's correlation at the
+// smallest levels (parity half of <= 6 rows: l0, l1 at 384x448; measured 6.8 / 7.8 us against
+// 11.0 / 13.4 us for corr_small + its reduce).  PWC_CORR_BAND=0 disables it, =1 forces it at
+// every size (measurement).
+static int band_mode() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = std::getenv("PWC_CORR_BAND");
+    v = (s && s[0] == '0') ? 0 : (s && s[0] == '1') ? 2 : 1;
+  }
+  return v;
+}
+
+hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void*, int, int, int,
+                              int, float, int, hipStream_t);
+
+hipError_t corr_forward_rows_f32(const void*, const void*, void*, int, int, int, int, float,
+                                 hipStream_t);
+
+// corr_rows.hip (row bands over full rows) serves l3-sized grids (it decides; PWC_ROWS).
+
 // PWC_CORR_GRP=0 disables the coarse-level kernel (measurement of the split path only).
 static bool grp_disabled() {
   static int v = -1;
@@ -523,6 +544,19 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
   const int D = 2 * dr + 1;
   const int max_splits = workspace ? corr_max_splits(B, D * D, Ho, Wo) : 1;
   if (max_splits <= 1) workspace = nullptr;
+  if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && layout == kRaster &&
+      s2 == 2 && pad == md && (md == 8 || md == 9) &&
+      (band_mode() == 2 || (band_mode() == 1 && (H + 1) / 2 <= 6))) {
+    const hipError_t e =
+        warp_corr_band_f32(in1, in2, nullptr, nullptr, out, B, C, H, W, divisor, 0, stream);
+    if (e != hipErrorNotSupported) return e;
+  }
+  if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && layout == kRaster &&
+      s2 == 2 && pad == md && (md == 8 || md == 9) &&
+      (uintptr_t)in1 % 16 == 0 && (uintptr_t)in2 % 16 == 0 && (uintptr_t)out % 16 == 0) {
+    const hipError_t e = corr_forward_rows_f32(in1, in2, out, B, C, H, W, divisor, stream);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4) {
     // stride-2 displacements with 16-B aligned rows (l2..l4 of PWC-Net): parity tiles
     // (corr_pt.hip), channel groups chosen by grid size

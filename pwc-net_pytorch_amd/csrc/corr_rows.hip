@@ -1,0 +1,313 @@
+// corr_rows.hip — correlation forward of model.py:24's configuration (pad == md in {8, 9},
+// k 1, s1 1, s2 2: 81 displacement channels, /C) for the larger pyramid levels, fp32, W % 4 == 0.
+//
+//   out[n, tj*9+ti, y, x] = sum_c f1[n,c,y,x] * f2[n,c,y+2tj-8,x+2ti-8] / C, zeros outside
+//   (correlation_cuda_kernel.cu:34-106 with kernel_size 1, stride1 1, stride2 2).
+//
+// Row-band decomposition.  Output row y only meets f2 rows of its own parity and output column
+// x only f2 columns of its own parity, so one workgroup owns
+//     one image  x  one row parity p  x  a band of R parity rows,   ALL 9 x 9 displacements,
+// over FULL rows: it reads the band's R f1 rows and the R + 8 same-parity f2 rows they meet
+// (1 + 8/R of the f2 bytes, no column halo: the zero columns of the reference's padding live in
+// LDS), channels streamed through LDS in chunks of CK.  Rows are fetched as 16-byte buffer
+// loads (one per lane, contiguous 448-B rows at l4) and split into even / odd columns on the
+// way into LDS (parity-column space, where the displacement step 2ti is 1 and every lane's
+// window is 3 aligned quads).  Rows outside the image come back as zeros from the buffer range
+// check, so no LDS clear is needed per chunk.
+//
+// Compute: item = (tj, row, column parity, 4-pixel segment); per channel 1 f1 quad + 3 f2
+// quads feed 36 FMAs (0.44 LDS floats per FMA).  G = NT / items channel groups meet in LDS in a
+// fixed order (deterministic).  The result block is written row by row as 16-byte
+// nontemporal stores (lane = 4 consecutive x).
+#include <hip/hip_ext.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "pwc_common.cuh"
+
+namespace pwc {
+
+void take_launch_events(hipEvent_t* start, hipEvent_t* stop);  // capi.hip
+
+namespace rows {
+
+constexpr int D = 9;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+struct Geo {
+  int Wq4;   // parity-column slots of an f1 row half (W/2 rounded up to 4)
+  int Wf;    // f2 row half slots: Wq4 + 8
+  int S;     // 4-pixel segments per row half
+  int Q;     // 16-byte quads per image row (W / 4)
+  int I;     // compute items: 9 * R * 2 * S
+  int G;     // channel groups
+  int nb;    // bands per parity half
+  int units; // B * 2 * nb
+  int ck;    // channels per chunk
+  int f1f;   // floats of one chunk's f1 image: ck * R * 2 * Wq4
+  int f2f;   // floats of one chunk's f2 image: ck * (R + 8) * 2 * Wf
+  float inv_Q, inv_NR2, inv_I, inv_S, inv_W4;
+};
+
+__device__ __forceinline__ int qdiv(int x, float inv) {
+  return (int)(((float)x + 0.5f) * inv);
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int R, int NT, int ML1, int ML2>
+__global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__ f1,
+                                                       const float* __restrict__ f2,
+                                                       float* __restrict__ out, int C, int H,
+                                                       int W, float divisor, float inv_divisor,
+                                                       Geo g) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NR2 = R + 8;
+  const int t = threadIdx.x;
+  const int unit = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring bands share an L2
+  const int b = unit % g.nb, np = unit / g.nb;
+  const int p = np & 1, n = np >> 1;
+  const int hp = (H - p + 1) >> 1;
+  const int r0 = b * R;
+  const uint32_t plane = (uint32_t)(H * W);
+  const uint32_t img_bytes = (uint32_t)C * plane * 4u;
+  const size_t img = (size_t)n * C * plane;
+  const __amdgpu_buffer_rsrc_t rs1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(f1 + img), (short)0, (int)img_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(f2 + img), (short)0, (int)img_bytes, 0x00020000);
+  float* f1s = lds;
+  float* f2s = lds + g.f1f;
+  constexpr uint32_t kOOB = 0x80000000u;
+
+  // zero the f2 pad slots once: 4 on the left of each row half, and from column W/2 to the end
+  // of the half on the right (Wq4 may exceed W/2); the row slots are rewritten every chunk
+  {
+    const int half_w = W >> 1;
+    const int nright = (g.Wf - 4 - half_w) >> 1;  // f32x2 pieces (W/2 is even)
+    const int per = 2 + nright;
+    const int npieces = g.ck * NR2 * 2 * per;
+    for (int i = t; i < npieces; i += NT) {
+      const int rh = i / per, e = i - rh * per;
+      const int col = e < 2 ? 2 * e : 4 + half_w + 2 * (e - 2);
+      *reinterpret_cast<f32x2*>(f2s + rh * g.Wf + col) = f32x2{0.f, 0.f};
+    }
+  }
+
+  // ---- per-thread staging plan (fixed over chunks).  f1 items = (channel, band row, quad),
+  // f2 items = (channel, f2 row, quad): two lists so each load names one buffer resource ----
+  const int tot1 = g.ck * R * g.Q, tot2 = g.ck * NR2 * g.Q;
+  uint32_t vo1[ML1], vo2[ML2];
+  int ld1[ML1], ld2[ML2], ch1[ML1], ch2[ML2];
+#pragma unroll
+  for (int j = 0; j < ML1; ++j) {
+    const int itm = t + j * NT;
+    const int rest = qdiv(itm, g.inv_Q), qd = itm - rest * g.Q;
+    const int c = rest / R, rho = rest - c * R;
+    const bool ok = itm < tot1 && r0 + rho < hp;
+    vo1[j] = ok ? ((uint32_t)c * plane + (uint32_t)(2 * (r0 + rho) + p) * W + 4 * qd) * 4u : kOOB;
+    ld1[j] = itm < tot1 ? ((c * R + rho) * 2) * g.Wq4 + 2 * qd : -1;
+    ch1[j] = c;
+  }
+#pragma unroll
+  for (int j = 0; j < ML2; ++j) {
+    const int itm = t + j * NT;
+    const int rest = qdiv(itm, g.inv_Q), qd = itm - rest * g.Q;
+    const int c = qdiv(rest, g.inv_NR2), k = rest - c * NR2;
+    const int rr = r0 - 4 + k;
+    const bool ok = itm < tot2 && rr >= 0 && rr < hp;
+    vo2[j] = ok ? ((uint32_t)c * plane + (uint32_t)(2 * rr + p) * W + 4 * qd) * 4u : kOOB;
+    ld2[j] = itm < tot2 ? g.f1f + ((c * NR2 + k) * 2) * g.Wf + 4 + 2 * qd : -1;
+    ch2[j] = c;
+  }
+
+  // ---- compute item ----
+  const int grp = qdiv(t, g.inv_I), it = t - grp * g.I;
+  const bool active = grp < g.G;
+  const int s = it - qdiv(it, g.inv_S) * g.S;
+  int rest = qdiv(it, g.inv_S);
+  const int q = rest & 1;
+  rest >>= 1;
+  const int r = rest % R, tt = rest / R;
+  const int a_off = (r * 2 + q) * g.Wq4 + 4 * s;
+  const int b_off = g.f1f + ((r + tt) * 2 + q) * g.Wf + 4 * s;
+  const int s1c = R * 2 * g.Wq4, s2c = NR2 * 2 * g.Wf;  // floats per channel
+  float acc[D][4];
+#pragma unroll
+  for (int ti = 0; ti < D; ++ti)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc[ti][kk] = 0.f;
+
+  for (int cb = 0; cb < C; cb += g.ck) {
+    const int cn = min(g.ck, C - cb);
+    const int so = (int)((uint32_t)cb * plane * 4u);
+    f32x4 v1[ML1], v2[ML2];
+#pragma unroll
+    for (int j = 0; j < ML1; ++j)  // channels past C (last chunk) read zeros: range check
+      v1[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rs1, (int)(ch1[j] < cn ? vo1[j] : kOOB), so, 0));
+#pragma unroll
+    for (int j = 0; j < ML2; ++j)
+      v2[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rs2, (int)(ch2[j] < cn ? vo2[j] : kOOB), so, 0));
+    if (cb > 0) lds_barrier();  // the previous chunk's compute is done with the staging
+#pragma unroll
+    for (int j = 0; j < ML1; ++j) {
+      if (ld1[j] < 0) continue;
+      *reinterpret_cast<f32x2*>(lds + ld1[j]) = f32x2{v1[j].x, v1[j].z};
+      *reinterpret_cast<f32x2*>(lds + ld1[j] + g.Wq4) = f32x2{v1[j].y, v1[j].w};
+    }
+#pragma unroll
+    for (int j = 0; j < ML2; ++j) {
+      if (ld2[j] < 0) continue;
+      *reinterpret_cast<f32x2*>(lds + ld2[j]) = f32x2{v2[j].x, v2[j].z};
+      *reinterpret_cast<f32x2*>(lds + ld2[j] + g.Wf) = f32x2{v2[j].y, v2[j].w};
+    }
+    lds_barrier();
+    if (active) {
+      const float* pa = f1s + a_off;
+      const float* pb = lds + b_off;
+      for (int c = grp; c < cn; c += g.G) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(pa + c * s1c);
+        const f32x4 q0 = *reinterpret_cast<const f32x4*>(pb + c * s2c);
+        const f32x4 q1 = *reinterpret_cast<const f32x4*>(pb + c * s2c + 4);
+        const f32x4 q2 = *reinterpret_cast<const f32x4*>(pb + c * s2c + 8);
+        const float w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                             q2.x, q2.y, q2.z, q2.w};
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int ti = 0; ti < D; ++ti)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) acc[ti][kk] = fmaf(av[kk], w[kk + ti], acc[ti][kk]);
+      }
+    }
+  }
+  lds_barrier();  // staging dead: partial sums reuse it
+  if (active) {
+    f32x4* rp = reinterpret_cast<f32x4*>(lds) + (grp * g.I + it) * D;
+#pragma unroll
+    for (int ti = 0; ti < D; ++ti) rp[ti] = f32x4{acc[ti][0], acc[ti][1], acc[ti][2], acc[ti][3]};
+  }
+  lds_barrier();
+
+  // ---- epilogue: lane = 4 consecutive x of one (tj, ti, row); fixed-order group sum ----
+  const int W4 = W >> 2;
+  const int nout = D * D * R * W4;
+  const int gstride = g.I * D * 4;
+  for (int o = t; o < nout; o += NT) {
+    const int m = o - qdiv(o, g.inv_W4) * W4;  // x = 4m .. 4m+3
+    int rr2 = qdiv(o, g.inv_W4);
+    const int rowi = rr2 % R;
+    rr2 /= R;
+    const int ti = rr2 % D, tj = rr2 / D;
+    const int row = r0 + rowi;
+    if (row >= hp) continue;
+    // x = 4m + e: parity e & 1, parity slot i = 2m + (e >> 1) -> segment s = i >> 2, kk = i & 3
+    const int i0 = 2 * m, sg = i0 >> 2, kk = i0 & 3;  // kk in {0, 2}
+    const int it0 = ((tj * R + rowi) * 2 + 0) * g.S + sg;
+    const int it1 = ((tj * R + rowi) * 2 + 1) * g.S + sg;
+    const float* p0 = lds + (it0 * D + ti) * 4 + kk;
+    const float* p1 = lds + (it1 * D + ti) * 4 + kk;
+    f32x2 e0 = *reinterpret_cast<const f32x2*>(p0);
+    f32x2 e1 = *reinterpret_cast<const f32x2*>(p1);
+    for (int gg = 1; gg < g.G; ++gg) {
+      e0 += *reinterpret_cast<const f32x2*>(p0 + gg * gstride);
+      e1 += *reinterpret_cast<const f32x2*>(p1 + gg * gstride);
+    }
+    f32x4 v4 = f32x4{e0.x, e1.x, e0.y, e1.y};
+    if (inv_divisor != 0.f)
+      v4 *= inv_divisor;
+    else
+      v4 = f32x4{v4.x / divisor, v4.y / divisor, v4.z / divisor, v4.w / divisor};
+    st_out4(out + ((size_t)(n * (D * D) + tj * D + ti) * H + (2 * row + p)) * W + 4 * m, v4);
+  }
+}
+
+}  // namespace rows
+
+// Serves l3-sized grids (13..24 parity rows per image) by default.  PWC_ROWS=0 disables the
+// kernel, PWC_ROWS=1 selects it at every size >= 13 parity rows, PWC_ROWS_CFG="R,CK" forces
+// a configuration at any size (measurement).
+hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, int B, int C,
+                                 int H, int W, float divisor, hipStream_t stream) {
+  using namespace rows;
+  static const int mode = [] {
+    const char* e = std::getenv("PWC_ROWS");
+    return (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 2 : 1;
+  }();
+  if (mode == 0) return hipErrorNotSupported;
+  if (W % 4 != 0 || W < 8 || B == 0) return hipErrorNotSupported;
+  if ((size_t)B * C * H * W >= (1ull << 30) || (size_t)B * 81 * H * W >= (1ull << 31))
+    return hipErrorNotSupported;
+  // measured (tools/gpu_rows.sh, B=8 384x448): l2 (12 parity rows) stays on corr_pt.hip,
+  // l3 (24) R 2 -> 14.4 us against 16.1, l4 (48) R 3 -> 18.5 against 19.4 (kbench)
+  const int hp0 = (H + 1) / 2;
+  int R = hp0 <= 24 ? 2 : 3, CK = 16;
+  if (const char* e = std::getenv("PWC_ROWS_CFG")) {
+    std::sscanf(e, "%d,%d", &R, &CK);
+  } else if (hp0 <= 12 || (hp0 > 24 && mode != 2)) {
+    return hipErrorNotSupported;
+  }
+  Geo g;
+  g.Wq4 = ((W / 2) + 3) & ~3;
+  g.Wf = g.Wq4 + 8;
+  g.S = g.Wq4 / 4;
+  g.Q = W / 4;
+  g.I = D * R * 2 * g.S;
+  constexpr int NT = 768;
+  if (g.I > NT || R < 1) return hipErrorNotSupported;
+  g.G = NT / g.I;
+  if (g.G > C) g.G = C;
+  const int hp = (H + 1) / 2;
+  g.nb = (hp + R - 1) / R;
+  g.units = B * 2 * g.nb;
+  g.ck = CK < C ? CK : C;
+  g.f1f = g.ck * R * 2 * g.Wq4;
+  g.f2f = g.ck * (R + 8) * 2 * g.Wf;
+  const size_t stage = (size_t)(g.f1f + g.f2f) * 4;
+  const size_t red = (size_t)g.G * g.I * D * 16;
+  const size_t lds = stage > red ? stage : red;
+  if (lds > 160 * 1024) return hipErrorNotSupported;
+  const int per1 = (g.ck * R * g.Q + NT - 1) / NT;
+  const int per2 = (g.ck * (R + 8) * g.Q + NT - 1) / NT;
+  g.inv_Q = 1.f / (float)g.Q;
+  g.inv_NR2 = 1.f / (float)(R + 8);
+  g.inv_I = 1.f / (float)g.I;
+  g.inv_S = 1.f / (float)g.S;
+  g.inv_W4 = 1.f / (float)(W / 4);
+  int ex;
+  const float mnt = std::frexp(divisor, &ex);
+  const float inv = (mnt == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  take_launch_events(&ev0, &ev1);
+#define PWC_ROWS(RR, M1, M2)                                                                  \
+  if (R == RR && per1 <= M1 && per2 <= M2) {                                                  \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      hipError_t e = hipFuncSetAttribute(                                                     \
+          reinterpret_cast<const void*>(&corr_fwd_rows<RR, NT, M1, M2>),                      \
+          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+      if (e != hipSuccess) return e;                                                          \
+      attr = true;                                                                            \
+    }                                                                                         \
+    hipExtLaunchKernelGGL((corr_fwd_rows<RR, NT, M1, M2>), dim3((unsigned)g.units), dim3(NT), \
+                          lds, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,     \
+                          (float*)out, C, H, W, divisor, inv, g);                             \
+    return hipGetLastError();                                                                 \
+  }
+  PWC_ROWS(3, 2, 7)   // l4 at CK 16: 1.75 / 6.4 loads per thread per chunk
+  PWC_ROWS(3, 1, 4)   // CK 8
+  PWC_ROWS(2, 2, 6)
+  PWC_ROWS(2, 1, 3)
+  PWC_ROWS(1, 1, 5)
+  PWC_ROWS(4, 2, 8)
+#undef PWC_ROWS
+  return hipErrorNotSupported;
+}
+
+}  // namespace pwc

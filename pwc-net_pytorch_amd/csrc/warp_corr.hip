@@ -451,8 +451,8 @@ hipError_t warp_corr_band_f32(const void* f1, const void* x2, const void* flow, 
       R = 3;  // l0: 7.7 us (warp 3.1 + correlation 10.9 unfused)
       T = 1;
     } else if (hp <= 6) {
-      R = 2;  // l1: 10.7 us (3.4 + 13.4 unfused)
-      T = 3;
+      R = 2;  // l1: fused 10.7 us (3.4 + 13.4 unfused); plain correlation 7.8 us with T = 1
+      T = warp ? 3 : 1;
     } else {
       R = 3;  // l2 and larger (the bench keeps l2..l4 unfused: 17.7 vs 3.6 + 11.4 us at l2)
       T = 3;

@@ -29,6 +29,8 @@ CORR_CASES = [
     (1, 96, 24, 28, 9, 1, 9, 1, 2),     # l2
     (1, 64, 48, 56, 9, 1, 9, 1, 2),     # l3
     (2, 32, 96, 112, 9, 1, 9, 1, 2),    # l4
+    (2, 40, 47, 52, 9, 1, 9, 1, 2),     # row bands: odd H, W/2 % 4 != 0, C % 16 != 0
+    (1, 20, 30, 36, 8, 1, 8, 1, 2),     # row bands, md = 8
     (1, 3, 17, 23, 9, 1, 9, 1, 2),      # ragged: W % 4 != 0, C % CC != 0
     (1, 5, 1, 1, 9, 1, 9, 1, 2),        # 1x1 image
     (2, 8, 12, 14, 4, 1, 4, 1, 1),      # Corr4
