@@ -153,6 +153,11 @@ __global__ void corr_bwd_generic(const T* __restrict__ in1, const T* __restrict_
   }
 }
 
+// corr_bwd_rows.hip: model.py:24's configuration (stride-2 displacements, pad == md), fp32.
+hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* gout, void* g1,
+                                  void* g2, int B, int C, int H, int W, float divisor,
+                                  hipStream_t stream);
+
 template <typename T>
 hipError_t corr_backward_t(const void* in1, const void* in2, const void* gout, void* g1,
                            void* g2, int B, int C, int H, int W, int Ho, int Wo, int pad, int k,
@@ -162,6 +167,12 @@ hipError_t corr_backward_t(const void* in1, const void* in2, const void* gout, v
   const int dr = md / s2;
   const size_t npix = (size_t)B * H * W;
   if (npix == 0 || C == 0) return hipSuccess;
+  if (force_generic == 0 && sizeof(T) == 4 && k == 1 && s1 == 1 && s2 == 2 && pad == md &&
+      (md == 8 || md == 9) && layout == kRaster) {
+    const hipError_t e = corr_backward_rows_f32(in1, in2, gout, g1, g2, B, C, H, W, divisor,
+                                                stream);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (force_generic != 1 && k == 1 && s1 == 1) {
     constexpr int CB = 8;
     const int off = md - pad;

@@ -1,0 +1,347 @@
+// corr_bwd_rows.hip — correlation backward of model.py:24's configuration (pad == md in {8, 9},
+// k 1, s1 1, s2 2: 81 displacement channels, /C), fp32, as row-band gathers (no atomics).
+//
+//   g1[n,c,y,x]   = sum_t gO[n,t,y,x] * f2[n,c,y+2tj-8,x+2ti-8] / C            (cu:108-198)
+//   g2[n,c,y',x'] = sum_t gO[n,t,y'-2tj+8,x'-2ti+8] * f1[n,c,y'-2tj+8,x'-2ti+8] / C
+//                                                                                (cu:200-290)
+// with t = tj*9 + ti and zero terms outside the image.  In parity space (y = 2Y+p, x = 2X+q)
+// both are 9x9 stencils over ONE parity image, the structure of the forward (corr_rows.hip):
+//   g1[c,Y,X]   = sum_{tj,ti} gO[t,Y,X]           * F2[c, Y+tj-4, X+ti-4]
+//   g2[c,Y',X'] = sum_{tj,ti} gO[t,Y'-tj+4,X'-ti+4] * F1[c, Y'-tj+4, X'-ti+4]
+// One workgroup owns one image x one row parity p x a band of R parity rows over full rows.
+// It stages the R + 8 same-parity feature rows of a chunk of channels in LDS (split into
+// column parities, 4 zero slots each side: the reference's zero padding), and each item
+// (tj, band row, column parity, 4-pixel segment) holds the 36 gO values it needs in
+// registers for the whole channel loop.  Per channel an item reads 3 aligned quads of one
+// staged row and runs 36 FMAs (the forward's ratio); the 9 tj partials of every (channel,
+// pixel) meet in LDS and are summed in tj order (deterministic), then stored row by row.
+// gO is read once per gradient; the staged features (R+8)/R times, mostly from L2.
+//
+// VEC (W % 4 == 0, 16-B aligned rows): 16-byte buffer loads split into column parities on the
+// way into LDS and 16-byte stores; otherwise dword loads/stores (any W, the l0/l1 levels).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "pwc_common.cuh"
+
+namespace pwc {
+namespace bwdrows {
+
+constexpr int D = 9;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kOOB = 0x80000000u;
+
+struct Geo {
+  int R;     // parity rows per band
+  int Wq4;   // slots of a staged row half: ceil(W/2) rounded up to 4
+  int Wf;    // Wq4 + 8 (4 zero slots on each side)
+  int S;     // 4-pixel segments per row half (Wq4 / 4)
+  int I;     // items: 9 * R * 2 * S
+  int G;     // channel groups
+  int ck;    // channels per chunk (CT * G)
+  int nb;    // bands per parity half
+  int stf;   // staging floats: ck * (R + 8) * 2 * Wf
+  int nld;   // staging load items per chunk: ck * (R + 8) * (W / 4 if VEC else W)
+  int lw;    // load items per staged row: W / 4 (VEC) or W
+  float inv_lw, inv_NR, inv_I, inv_S, inv_R;
+};
+
+__device__ __forceinline__ int qdiv(int x, float inv) { return (int)(((float)x + 0.5f) * inv); }
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ float ld1(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0));
+}
+__device__ __forceinline__ f32x4 ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+}
+
+// GRAD 1: feat = f2, result g1.  GRAD 2: feat = f1, result g2.  CT channels per item and
+// chunk, ML staging loads per thread and chunk.
+template <int GRAD, bool VEC, int CT, int ML, int NT>
+__global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__ feat,
+                                                       const float* __restrict__ gout,
+                                                       float* __restrict__ gin, int C, int H,
+                                                       int W, float divisor, float inv_divisor,
+                                                       Geo g) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* stg = lds;
+  f32x4* part = reinterpret_cast<f32x4*>(lds + g.stf);
+  const int t = threadIdx.x;
+  const int R = g.R, NR = R + 8;
+  const int unit = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring bands share an L2
+  const int b = unit % g.nb, np = unit / g.nb;
+  const int p = np & 1, n = np >> 1;
+  const int hp = (H - p + 1) >> 1;
+  const int r0 = b * R;
+  if (r0 >= hp) return;  // odd H: the odd-row half has one row fewer (uniform per workgroup)
+  const uint32_t plane = (uint32_t)(H * W);
+  const __amdgpu_buffer_rsrc_t rsf = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(feat + (size_t)n * C * plane), (short)0, (int)((uint32_t)C * plane * 4u),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t rsg = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(gout + (size_t)n * (D * D) * plane), (short)0,
+      (int)((uint32_t)(D * D) * plane * 4u), 0x00020000);
+
+  // zero the whole staging once: pad slots and the columns past each half's width stay zero
+  for (int i = t; i < g.stf / 4; i += NT) reinterpret_cast<f32x4*>(stg)[i] = f32x4{0, 0, 0, 0};
+
+  // ---- staging plan (fixed over chunks): item = (channel, staged row, raster quad/col) ----
+  uint32_t vo[ML];
+  int ls[ML], lc[ML];
+#pragma unroll
+  for (int j = 0; j < ML; ++j) {
+    const int itm = t + j * NT;
+    const int rest = qdiv(itm, g.inv_lw), e = itm - rest * g.lw;
+    const int c = qdiv(rest, g.inv_NR), k = rest - c * NR;
+    const int rr = r0 - 4 + k;
+    const bool ok = itm < g.nld && rr >= 0 && rr < hp;
+    const int col = VEC ? 4 * e : e;
+    vo[j] = ok ? ((uint32_t)c * plane + (uint32_t)(2 * rr + p) * W + col) * 4u : kOOB;
+    // VEC: slot 4 + 2e of both halves; scalar: half e & 1, slot 4 + (e >> 1)
+    ls[j] = itm < g.nld ? ((c * NR + k) * 2 + (VEC ? 0 : (e & 1))) * g.Wf + 4 +
+                              (VEC ? 2 * e : (e >> 1))
+                        : -1;
+    lc[j] = c;
+  }
+
+  // ---- compute item (tj, band row r, column parity q, segment s) ----
+  const int grp = qdiv(t, g.inv_I), it = t - grp * g.I;
+  const bool active = grp < g.G;
+  const int s = it - qdiv(it, g.inv_S) * g.S;
+  int rest = qdiv(it, g.inv_S);
+  const int q = rest & 1;
+  rest >>= 1;
+  const int r = rest - qdiv(rest, g.inv_R) * R, tj = qdiv(rest, g.inv_R);
+  const int whq = (W - q + 1) >> 1;  // columns of this parity
+  // the 36 gO values of this item, zero where the forward output does not exist
+  float gv[D][4];
+  {
+    const int Y = GRAD == 1 ? r0 + r : r0 + r - tj + 4;  // gO parity row
+    const bool rok = active && Y >= 0 && Y < hp && r0 + r < hp;
+#pragma unroll
+    for (int ti = 0; ti < D; ++ti) {
+      const int X0 = GRAD == 1 ? 4 * s : 4 * s - ti + 4;  // gO parity column of kk = 0
+      const uint32_t rowoff = (uint32_t)(tj * D + ti) * plane + (uint32_t)(2 * Y + p) * W;
+      if (VEC && GRAD == 1) {
+        const uint32_t o = rok ? (rowoff + 8 * s) * 4u : kOOB;
+        const f32x4 a = ld4(rsg, o), c4 = ld4(rsg, o + 16u);
+        gv[ti][0] = q ? a.y : a.x;
+        gv[ti][1] = q ? a.w : a.z;
+        gv[ti][2] = q ? c4.y : c4.x;
+        gv[ti][3] = q ? c4.w : c4.z;
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int X = X0 + kk;
+          const bool ok = rok && X >= 0 && X < whq;
+          gv[ti][kk] = ld1(rsg, ok ? (rowoff + 2 * X + q) * 4u : kOOB);
+        }
+      }
+    }
+  }
+  const int krow = GRAD == 1 ? r + tj : r - tj + 8;  // staged feature row
+  const int wbase = (krow * 2 + q) * g.Wf + 4 * s;
+  const int cstride = NR * 2 * g.Wf;
+  const int RS2 = R * 2 * g.S;
+  const int pbase = (tj * R + r) * 2 * g.S + q * g.S + s;
+
+  for (int cb = 0; cb < C; cb += g.ck) {
+    const int cn = min(g.ck, C - cb);
+    const uint32_t so = (uint32_t)cb * plane * 4u;
+    if (VEC) {
+      f32x4 v[ML];
+#pragma unroll
+      for (int j = 0; j < ML; ++j) v[j] = ld4(rsf, (lc[j] < cn ? vo[j] : kOOB) + so);
+      lds_barrier();  // the zeroing / the previous chunk's compute and epilogue are done
+#pragma unroll
+      for (int j = 0; j < ML; ++j) {
+        if (ls[j] < 0) continue;
+        *reinterpret_cast<f32x2*>(stg + ls[j]) = f32x2{v[j].x, v[j].z};
+        *reinterpret_cast<f32x2*>(stg + ls[j] + g.Wf) = f32x2{v[j].y, v[j].w};
+      }
+    } else {
+      float v[ML];
+#pragma unroll
+      for (int j = 0; j < ML; ++j) v[j] = ld1(rsf, (lc[j] < cn ? vo[j] : kOOB) + so);
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < ML; ++j)
+        if (ls[j] >= 0) stg[ls[j]] = v[j];
+    }
+    lds_barrier();
+    if (active) {
+#pragma unroll
+      for (int j = 0; j < CT; ++j) {
+        const int c = grp + j * g.G;  // channel within the chunk (< ck)
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        if (c < cn) {
+          const float* pw = stg + c * cstride + wbase;
+          const f32x4 q0 = *reinterpret_cast<const f32x4*>(pw);
+          const f32x4 q1 = *reinterpret_cast<const f32x4*>(pw + 4);
+          const f32x4 q2 = *reinterpret_cast<const f32x4*>(pw + 8);
+          const float w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y,
+                               q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+#pragma unroll
+          for (int ti = 0; ti < D; ++ti)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+              acc[kk] = fmaf(gv[ti][kk], w[GRAD == 1 ? kk + ti : kk + 8 - ti], acc[kk]);
+        }
+        part[c * (D * RS2) + pbase] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+      }
+    }
+    lds_barrier();
+    // ---- epilogue: the 9 tj partials of each (channel, pixel) summed in tj order ----
+    if (VEC) {
+      const int Q = W >> 2;
+      const int nout = cn * R * Q;
+      for (int o = t; o < nout; o += NT) {
+        const int m = o - qdiv(o, g.inv_lw) * Q;  // raster quad: x = 4m .. 4m+3
+        const int rc = qdiv(o, g.inv_lw);
+        const int rr = rc - qdiv(rc, g.inv_R) * R, c = qdiv(rc, g.inv_R);
+        if (r0 + rr >= hp) continue;
+        const int i0 = 2 * m, sg = i0 >> 2, kk = i0 & 3;  // kk in {0, 2}
+        const float* p0 =
+            reinterpret_cast<const float*>(part + c * (D * RS2) + rr * 2 * g.S + sg) + kk;
+        const float* p1 = p0 + 4 * g.S;  // column parity 1
+        f32x2 e0 = *reinterpret_cast<const f32x2*>(p0);
+        f32x2 e1 = *reinterpret_cast<const f32x2*>(p1);
+#pragma unroll
+        for (int j = 1; j < D; ++j) {
+          e0 += *reinterpret_cast<const f32x2*>(p0 + 4 * j * RS2);
+          e1 += *reinterpret_cast<const f32x2*>(p1 + 4 * j * RS2);
+        }
+        f32x4 v4 = f32x4{e0.x, e1.x, e0.y, e1.y};
+        if (inv_divisor != 0.f)
+          v4 *= inv_divisor;
+        else
+          v4 = f32x4{v4.x / divisor, v4.y / divisor, v4.z / divisor, v4.w / divisor};
+        st_out4(gin + ((size_t)n * C + cb + c) * plane + (size_t)(2 * (r0 + rr) + p) * W +
+                    4 * m,
+                v4);
+      }
+    } else {
+      const int nout = cn * R * W;
+      for (int o = t; o < nout; o += NT) {
+        const int x = o - qdiv(o, g.inv_lw) * W;
+        const int rc = qdiv(o, g.inv_lw);
+        const int rr = rc - qdiv(rc, g.inv_R) * R, c = qdiv(rc, g.inv_R);
+        if (r0 + rr >= hp) continue;
+        const int qq = x & 1, X = x >> 1;
+        const float* p0 = reinterpret_cast<const float*>(part + c * (D * RS2) + rr * 2 * g.S +
+                                                         qq * g.S + (X >> 2)) +
+                          (X & 3);
+        float e = *p0;
+#pragma unroll
+        for (int j = 1; j < D; ++j) e += p0[4 * j * RS2];
+        e = inv_divisor != 0.f ? e * inv_divisor : e / divisor;
+        st_out1(gin + ((size_t)n * C + cb + c) * plane + (size_t)(2 * (r0 + rr) + p) * W + x, e);
+      }
+    }
+  }
+}
+
+}  // namespace bwdrows
+
+// PWC_BWD_ROWS=0 disables the kernel; PWC_BWD_CFG="R,CT" forces a band height and channels per
+// item (measurement).
+hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* gout, void* g1,
+                                  void* g2, int B, int C, int H, int W, float divisor,
+                                  hipStream_t stream) {
+  using namespace bwdrows;
+  static const bool off = [] {
+    const char* e = std::getenv("PWC_BWD_ROWS");
+    return e && e[0] == '0';
+  }();
+  if (off || B == 0 || C == 0 || H == 0 || W < 2) return hipErrorNotSupported;
+  if ((size_t)C * H * W >= (1ull << 29) || (size_t)81 * H * W >= (1ull << 29))
+    return hipErrorNotSupported;
+  const bool vec = W % 4 == 0 && (uintptr_t)in1 % 16 == 0 && (uintptr_t)in2 % 16 == 0 &&
+                   (uintptr_t)gout % 16 == 0 && (uintptr_t)g1 % 16 == 0 &&
+                   (uintptr_t)g2 % 16 == 0;
+  constexpr int NT = 768;
+  const int hp = (H + 1) / 2;
+  Geo g;
+  g.Wq4 = (((W + 1) / 2) + 3) & ~3;
+  g.Wf = g.Wq4 + 8;
+  g.S = g.Wq4 / 4;
+  // the tallest band (least restaging of the R + 8 feature rows) that still gives about one
+  // workgroup per CU
+  int R = 1, CT = 4;
+  for (int r : {3, 2, 1}) {
+    if (9 * r * 2 * g.S > NT) continue;
+    R = r;
+    if ((long long)B * 2 * ((hp + r - 1) / r) >= 240) break;
+  }
+  if (const char* e = std::getenv("PWC_BWD_CFG")) std::sscanf(e, "%d,%d", &R, &CT);
+  g.R = R;
+  g.I = 9 * R * 2 * g.S;
+  if (R < 1 || g.I > NT) return hipErrorNotSupported;
+  g.G = NT / g.I;
+  if (g.G * CT > C) g.G = (C + CT - 1) / CT;
+  g.nb = (hp + R - 1) / R;
+  size_t lds = 0;
+  for (;; --g.G) {  // fewest channel groups' worth of LDS that fits
+    g.ck = CT * g.G;
+    g.stf = g.ck * (R + 8) * 2 * g.Wf;
+    lds = (size_t)g.stf * 4 + (size_t)g.ck * 9 * R * 2 * g.S * 16;
+    if (lds <= 160 * 1024) break;
+    if (g.G == 1) return hipErrorNotSupported;
+  }
+  g.lw = vec ? W / 4 : W;
+  g.nld = g.ck * (R + 8) * g.lw;
+  g.inv_lw = 1.f / (float)g.lw;
+  g.inv_NR = 1.f / (float)(R + 8);
+  g.inv_I = 1.f / (float)g.I;
+  g.inv_S = 1.f / (float)g.S;
+  g.inv_R = 1.f / (float)R;
+  const int ml = (g.nld + NT - 1) / NT;
+  int ex;
+  const float mnt = std::frexp(divisor, &ex);
+  const float inv = (mnt == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
+  const unsigned units = (unsigned)(B * 2 * g.nb);
+#define PWC_BWD(V, CTT, M)                                                                     \
+  if (vec == V && CT == CTT && ml <= M) {                                                      \
+    static bool attr = false;                                                                  \
+    if (!attr) {                                                                               \
+      hipError_t e = hipFuncSetAttribute(                                                      \
+          reinterpret_cast<const void*>(&corr_bwd_rows<1, V, CTT, M, NT>),                     \
+          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                             \
+      if (e == hipSuccess)                                                                     \
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_bwd_rows<2, V, CTT, M, NT>), \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
+      if (e != hipSuccess) return e;                                                           \
+      attr = true;                                                                             \
+    }                                                                                          \
+    hipLaunchKernelGGL((corr_bwd_rows<1, V, CTT, M, NT>), dim3(units), dim3(NT), lds, stream,  \
+                       (const float*)in2, (const float*)gout, (float*)g1, C, H, W, divisor,    \
+                       inv, g);                                                                \
+    hipError_t e = hipGetLastError();                                                          \
+    if (e != hipSuccess) return e;                                                             \
+    hipLaunchKernelGGL((corr_bwd_rows<2, V, CTT, M, NT>), dim3(units), dim3(NT), lds, stream,  \
+                       (const float*)in1, (const float*)gout, (float*)g2, C, H, W, divisor,    \
+                       inv, g);                                                                \
+    return hipGetLastError();                                                                  \
+  }
+  PWC_BWD(true, 4, 2)
+  PWC_BWD(true, 4, 4)
+  PWC_BWD(true, 4, 8)
+  PWC_BWD(true, 2, 4)
+  PWC_BWD(true, 8, 4)
+  PWC_BWD(false, 4, 4)
+  PWC_BWD(false, 4, 8)
+  PWC_BWD(false, 4, 16)
+  PWC_BWD(false, 2, 8)
+#undef PWC_BWD
+  return hipErrorNotSupported;
+}
+
+}  // namespace pwc

@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--levels", default="0,1,2,3,4")
     ap.add_argument("--ops", default="corr,warp,fused")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--flow-scale", type=float, default=2.0, help="flows ~ N(0, scale^2) px")
     ap.add_argument("--sets", type=int, default=0, help="buffer sets (0 = past the MALL)")
     args = ap.parse_args()
     dt = torch.float32 if args.dtype == "fp32" else torch.float16
@@ -76,7 +77,7 @@ def main():
         g = torch.Generator(device=dev).manual_seed(l)
         sets = [dict(x1=torch.randn(B, C, h, w, device=dev, generator=g).to(dt),
                      x2=torch.randn(B, C, h, w, device=dev, generator=g).to(dt),
-                     fl=(torch.randn(B, 2, h, w, device=dev, generator=g) * 2).to(dt))
+                     fl=(torch.randn(B, 2, h, w, device=dev, generator=g) * args.flow_scale).to(dt))
                 for _ in range(n)]
         ops = args.ops.split(",")
         cb = bench.corr_bytes_per_pair(C, h, w, esz) * B
