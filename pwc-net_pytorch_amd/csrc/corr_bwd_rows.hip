@@ -21,6 +21,7 @@
 // way into LDS and 16-byte stores; otherwise dword loads/stores (any W, the l0/l1 levels).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -46,6 +47,7 @@ struct Geo {
   int nb;    // bands per parity half
   int stf;   // staging floats: ck * (R + 8) * 2 * Wf
   int nld;   // staging load items per chunk: ck * (R + 8) * (W / 4 if VEC else W)
+  int cps;   // channels per slice (grid.y), a multiple of ck
   int lw;    // load items per staged row: W / 4 (VEC) or W
   float inv_lw, inv_NR, inv_I, inv_S, inv_R;
 };
@@ -153,29 +155,38 @@ __global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__
   const int RS2 = R * 2 * g.S;
   const int pbase = (tj * R + r) * 2 * g.S + q * g.S + s;
 
-  for (int cb = 0; cb < C; cb += g.ck) {
-    const int cn = min(g.ck, C - cb);
+  // channel slice of this workgroup (grid.y), chunks of ck; the next chunk's staging loads
+  // are in flight during the current chunk's compute and epilogue
+  const int cs = blockIdx.y * g.cps, ce = min(C, cs + g.cps);
+  f32x4 vv[ML];
+  float vs[ML];
+  auto issue = [&](int cb) {
+    const int cn = min(g.ck, ce - cb);
     const uint32_t so = (uint32_t)cb * plane * 4u;
-    if (VEC) {
-      f32x4 v[ML];
 #pragma unroll
-      for (int j = 0; j < ML; ++j) v[j] = ld4(rsf, (lc[j] < cn ? vo[j] : kOOB) + so);
-      lds_barrier();  // the zeroing / the previous chunk's compute and epilogue are done
-#pragma unroll
-      for (int j = 0; j < ML; ++j) {
-        if (ls[j] < 0) continue;
-        *reinterpret_cast<f32x2*>(stg + ls[j]) = f32x2{v[j].x, v[j].z};
-        *reinterpret_cast<f32x2*>(stg + ls[j] + g.Wf) = f32x2{v[j].y, v[j].w};
-      }
-    } else {
-      float v[ML];
-#pragma unroll
-      for (int j = 0; j < ML; ++j) v[j] = ld1(rsf, (lc[j] < cn ? vo[j] : kOOB) + so);
-      lds_barrier();
-#pragma unroll
-      for (int j = 0; j < ML; ++j)
-        if (ls[j] >= 0) stg[ls[j]] = v[j];
+    for (int j = 0; j < ML; ++j) {
+      const uint32_t o = (lc[j] < cn ? vo[j] : kOOB) + so;
+      if (VEC)
+        vv[j] = ld4(rsf, o);
+      else
+        vs[j] = ld1(rsf, o);
     }
+  };
+  if (cs < ce) issue(cs);
+  for (int cb = cs; cb < ce; cb += g.ck) {
+    const int cn = min(g.ck, ce - cb);
+    lds_barrier();  // the zeroing / the previous chunk's compute and epilogue are done
+#pragma unroll
+    for (int j = 0; j < ML; ++j) {
+      if (ls[j] < 0) continue;
+      if (VEC) {
+        *reinterpret_cast<f32x2*>(stg + ls[j]) = f32x2{vv[j].x, vv[j].z};
+        *reinterpret_cast<f32x2*>(stg + ls[j] + g.Wf) = f32x2{vv[j].y, vv[j].w};
+      } else {
+        stg[ls[j]] = vs[j];
+      }
+    }
+    if (cb + g.ck < ce) issue(cb + g.ck);
     lds_barrier();
     if (active) {
 #pragma unroll
@@ -273,13 +284,14 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   g.Wq4 = (((W + 1) / 2) + 3) & ~3;
   g.Wf = g.Wq4 + 8;
   g.S = g.Wq4 / 4;
-  // the tallest band (least restaging of the R + 8 feature rows) that still gives about one
-  // workgroup per CU
-  int R = 1, CT = 4;
+  // the tallest band (least restaging of the R + 8 feature rows); channel slices fill the chip
+  // CT 8 measured 17.2 against 22.9 us (4) at l2, equal at l3/l4; 4 on the dword path (l0/l1:
+  // 17.2 / 18.5 against 20.1 / 21.8 us)
+  int R = 1, CT = vec ? 8 : 4;
   for (int r : {3, 2, 1}) {
     if (9 * r * 2 * g.S > NT) continue;
     R = r;
-    if ((long long)B * 2 * ((hp + r - 1) / r) >= 240) break;
+    break;
   }
   if (const char* e = std::getenv("PWC_BWD_CFG")) std::sscanf(e, "%d,%d", &R, &CT);
   g.R = R;
@@ -298,6 +310,15 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   }
   g.lw = vec ? W / 4 : W;
   g.nld = g.ck * (R + 8) * g.lw;
+  // channel slices (grid.y) up to about one workgroup per CU: the slices of a band are
+  // independent (every gradient element is one channel's) but each re-reads the band's gO
+  const long long bands = (long long)B * 2 * ((hp + R - 1) / R);
+  const int nchunks = (C + g.ck - 1) / g.ck;
+  int nsl = 1;
+  while (nsl < nchunks && bands * (nsl + 1) <= 320) ++nsl;  // measured: 1 at l4, 2 at l3
+  if (const char* e = std::getenv("PWC_BWD_SLICES")) nsl = std::max(1, std::min(nchunks, std::atoi(e)));
+  g.cps = ((nchunks + nsl - 1) / nsl) * g.ck;
+  nsl = (C + g.cps - 1) / g.cps;
   g.inv_lw = 1.f / (float)g.lw;
   g.inv_NR = 1.f / (float)(R + 8);
   g.inv_I = 1.f / (float)g.I;
@@ -321,25 +342,27 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
       if (e != hipSuccess) return e;                                                           \
       attr = true;                                                                             \
     }                                                                                          \
-    hipLaunchKernelGGL((corr_bwd_rows<1, V, CTT, M, NT>), dim3(units), dim3(NT), lds, stream,  \
+    hipLaunchKernelGGL((corr_bwd_rows<1, V, CTT, M, NT>), dim3(units, nsl), dim3(NT), lds, stream, \
                        (const float*)in2, (const float*)gout, (float*)g1, C, H, W, divisor,    \
                        inv, g);                                                                \
     hipError_t e = hipGetLastError();                                                          \
     if (e != hipSuccess) return e;                                                             \
-    hipLaunchKernelGGL((corr_bwd_rows<2, V, CTT, M, NT>), dim3(units), dim3(NT), lds, stream,  \
+    hipLaunchKernelGGL((corr_bwd_rows<2, V, CTT, M, NT>), dim3(units, nsl), dim3(NT), lds, stream, \
                        (const float*)in1, (const float*)gout, (float*)g2, C, H, W, divisor,    \
                        inv, g);                                                                \
     return hipGetLastError();                                                                  \
   }
+  PWC_BWD(true, 8, 2)
+  PWC_BWD(true, 8, 4)
+  PWC_BWD(true, 8, 8)
   PWC_BWD(true, 4, 2)
   PWC_BWD(true, 4, 4)
   PWC_BWD(true, 4, 8)
-  PWC_BWD(true, 2, 4)
-  PWC_BWD(true, 8, 4)
-  PWC_BWD(false, 4, 4)
+  PWC_BWD(false, 8, 8)
+  PWC_BWD(false, 8, 16)
+  PWC_BWD(false, 8, 32)
   PWC_BWD(false, 4, 8)
   PWC_BWD(false, 4, 16)
-  PWC_BWD(false, 2, 8)
 #undef PWC_BWD
   return hipErrorNotSupported;
 }

@@ -166,6 +166,217 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   gflow[(2 * n + 1) * plane + pix] = (giy * my) / halfy;
 }
 
+// ---- backward without a scatter over HBM (fp32) ----
+// grad_x as a gather: a workgroup owns a TH x TW tile of grad_x (one pixel per thread) for
+// CC channels.  Every output pixel within M of the tile (its candidate window) recomputes its
+// sample (the forward's chain) and keeps the corners that fall in the tile; a counting sort in
+// LDS turns these into one list of (source pixel, bilinear weight) per tile pixel, sorted by
+// source pixel (deterministic).  Per channel a thread then sums gO * weight over its list in
+// registers and writes its grad_x element with a plain coalesced store: every element is
+// written once (no memset, no atomics, fixed summation order).  A corner whose pixel lies
+// outside the corner tile's candidate window (flow beyond ~M pixels) is left to
+// warp_bwd_flow, which adds it with a global atomic after this kernel (ATen's
+// grid_sampler_2d_backward adds every corner that way).
+constexpr int kBwdM = 8;
+
+__device__ __forceinline__ bool bwd_in_window(int py, int px, int cy, int cx, int th, int tw) {
+  const int ty0 = (cy / th) * th, tx0 = (cx / tw) * tw;
+  return py >= ty0 - kBwdM && py < ty0 + th + kBwdM && px >= tx0 - kBwdM &&
+         px < tx0 + tw + kBwdM;
+}
+
+template <int TW, int CC>
+__global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict__ flow,
+                                                         const float* __restrict__ gout,
+                                                         float* __restrict__ gx, int C, int H,
+                                                         int W, float halfx, float halfy,
+                                                         int ntx) {
+  constexpr int TH = 256 / TW, M = kBwdM;
+  constexpr int WW = TW + 2 * M, NCAND = (TH + 2 * M) * WW, K = (NCAND + 255) / 256;
+  constexpr int MAXL = 4 * NCAND;
+  __shared__ int cnt[256];
+  __shared__ int wsum[4];
+  __shared__ unsigned lpix[MAXL];
+  __shared__ float lw[MAXL];
+  const int t = threadIdx.x;
+  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const int n = blockIdx.y, c0 = blockIdx.z * CC;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const unsigned plane = (unsigned)(H * W);
+  cnt[t] = 0;
+  int slot[K][4];
+  float wt[K][4];
+  unsigned pix[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int cand = t + j * 256;
+    const int py = y0 - M + cand / WW, px = x0 - M + cand % WW;
+    pix[j] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) slot[j][k] = -1, wt[j][k] = 0.f;
+    if (cand >= NCAND || py < 0 || py >= H || px < 0 || px >= W) continue;
+    pix[j] = (unsigned)(py * W + px);
+    const float u = flow[(2 * n + 0) * plane + pix[j]];
+    const float v = flow[(2 * n + 1) * plane + pix[j]];
+    const Bilinear b = bilinear(src_coord(u, px, W, halfx), src_coord(v, py, H, halfy), H, W);
+    const float w[4] = {b.wx0 * b.wy0, b.wx1 * b.wy0, b.wx0 * b.wy1, b.wx1 * b.wy1};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cy = b.y0 + (k >> 1), cx = b.x0 + (k & 1);
+      if (cy >= 0 && cy < H && cx >= 0 && cx < W && cy >= y0 && cy < y0 + TH && cx >= x0 &&
+          cx < x0 + TW) {
+        slot[j][k] = (cy - y0) * TW + (cx - x0);
+        wt[j][k] = w[k];
+      }
+    }
+  }
+  __syncthreads();
+  // counting sort by tile pixel
+  int pos[K][4];
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pos[j][k] = slot[j][k] >= 0 ? atomicAdd(&cnt[slot[j][k]], 1) : 0;
+  __syncthreads();
+  const int len = cnt[t];
+  int incl = len;  // inclusive scan: within the wave, then over the 4 waves
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(incl, d, 64);
+    if ((t & 63) >= d) incl += o;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = incl;
+  __syncthreads();
+  for (int w = 0; w < (t >> 6); ++w) incl += wsum[w];
+  const int start = incl - len;
+  cnt[t] = start;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (slot[j][k] >= 0) {
+        const int e = cnt[slot[j][k]] + pos[j][k];
+        lpix[e] = pix[j];
+        lw[e] = wt[j][k];
+      }
+  __syncthreads();
+  // my list, sorted by source pixel (insertion sort: a few entries)
+  for (int i = start + 1; i < start + len; ++i) {
+    const unsigned pk = lpix[i];
+    const float wk = lw[i];
+    int j = i - 1;
+    while (j >= start && lpix[j] > pk) {
+      lpix[j + 1] = lpix[j];
+      lw[j + 1] = lw[j];
+      --j;
+    }
+    lpix[j + 1] = pk;
+    lw[j + 1] = wk;
+  }
+  const int yy = y0 + t / TW, xx = x0 + t % TW;
+  if (yy >= H || xx >= W) return;
+  const int cn = min(CC, C - c0);
+  const float* go = gout + ((unsigned)(n * C + c0)) * plane;
+  float acc[CC];
+#pragma unroll
+  for (int i = 0; i < CC; ++i) acc[i] = 0.f;
+  for (int e = start; e < start + len; ++e) {
+    const unsigned p = lpix[e];
+    const float w = lw[e];
+    float g[CC];
+#pragma unroll
+    for (int i = 0; i < CC; ++i) g[i] = go[(unsigned)min(i, cn - 1) * plane + p];
+#pragma unroll
+    for (int i = 0; i < CC; ++i) acc[i] += g[i] * w;
+  }
+  float* o = gx + ((unsigned)(n * C + c0)) * plane + (unsigned)(yy * W + xx);
+#pragma unroll
+  for (int i = 0; i < CC; ++i)
+    if (i < cn) o[(unsigned)i * plane] = acc[i];
+}
+
+// grad_flow per pixel + the corners warp_bwd_gx_lists left out.  A block holds 256 / NG
+// pixels x NG channel groups (lanes of a wave = consecutive pixels of one group); group g
+// takes channels [g*cpg, (g+1)*cpg) and the NG partial sums meet in LDS in group order
+// (deterministic; NG = 1 is ATen's channel loop order).
+template <int CB, int NG>
+__global__ __launch_bounds__(256) void warp_bwd_flow(const float* __restrict__ x,
+                                                     const float* __restrict__ flow,
+                                                     const float* __restrict__ gout,
+                                                     float* __restrict__ gx,
+                                                     float* __restrict__ gflow, int B, int C,
+                                                     int H, int W, float halfx, float halfy,
+                                                     int cpg, int th, int tw) {
+  constexpr int PX = 256 / NG;
+  __shared__ float red[NG > 1 ? 2 * 256 : 1];
+  const unsigned plane = (unsigned)(H * W);
+  const int grp = threadIdx.x / PX, pl = threadIdx.x - grp * PX;
+  const unsigned idx = xcd_remap(blockIdx.x, gridDim.x) * (unsigned)PX + pl;
+  const bool live = idx < (unsigned)B * plane;
+  if (NG == 1 && !live) return;
+  const unsigned idc = live ? idx : 0u;  // idle lanes of the last block sample pixel 0
+  const unsigned n = idc / plane;
+  const unsigned pix = idc - n * plane;
+  const int py = (int)(pix / (unsigned)W);
+  const int px = (int)pix - py * W;
+  const float u = flow[(2 * n + 0) * plane + pix];
+  const float v = flow[(2 * n + 1) * plane + pix];
+  const float ix = src_coord(u, px, W, halfx);
+  const float iy = src_coord(v, py, H, halfy);
+  const Bilinear b = bilinear(ix, iy, H, W);
+  const Corners k = corners(b, H, W);
+  const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;
+  const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
+  // corners outside their tile's candidate window (rare: |flow| beyond ~kBwdM)
+  const bool o00 = k.m00 != 0.f && !bwd_in_window(py, px, b.y0, b.x0, th, tw);
+  const bool o01 = k.m01 != 0.f && !bwd_in_window(py, px, b.y0, b.x0 + 1, th, tw);
+  const bool o10 = k.m10 != 0.f && !bwd_in_window(py, px, b.y0 + 1, b.x0, th, tw);
+  const bool o11 = k.m11 != 0.f && !bwd_in_window(py, px, b.y0 + 1, b.x0 + 1, th, tw);
+  const bool outl = o00 || o01 || o10 || o11;
+  float gix = 0.f, giy = 0.f;
+  const int cs = grp * cpg, ce = live ? min(C, cs + cpg) : cs;
+  for (int c0 = cs; c0 < ce; c0 += CB) {
+    float r[CB][4], go[CB];
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = min(c0 + i, ce - 1);
+      const float* p = x + ((unsigned)(n * C + c)) * plane;
+      r[i][0] = masked(p[k.i00], k.m00);
+      r[i][1] = masked(p[k.i01], k.m01);
+      r[i][2] = masked(p[k.i10], k.m10);
+      r[i][3] = masked(p[k.i11], k.m11);
+      go[i] = (c0 + i < ce) ? gout[((unsigned)(n * C + c)) * plane + pix] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      if (c0 + i >= ce) break;
+      if (outl) {
+        float* q = gx + ((unsigned)(n * C + c0 + i)) * plane;
+        if (o00) atomicAdd(q + k.i00, go[i] * w00);
+        if (o01) atomicAdd(q + k.i01, go[i] * w01);
+        if (o10) atomicAdd(q + k.i10, go[i] * w10);
+        if (o11) atomicAdd(q + k.i11, go[i] * w11);
+      }
+      gix += go[i] * ((r[i][1] - r[i][0]) * b.wy0 + (r[i][3] - r[i][2]) * b.wy1);
+      giy += go[i] * ((r[i][2] - r[i][0]) * b.wx0 + (r[i][3] - r[i][1]) * b.wx1);
+    }
+  }
+  if (NG > 1) {
+    red[threadIdx.x] = gix;
+    red[256 + threadIdx.x] = giy;
+    __syncthreads();
+    if (grp != 0 || !live) return;
+    for (int j = 1; j < NG; ++j) {
+      gix += red[j * PX + pl];
+      giy += red[256 + j * PX + pl];
+    }
+  }
+  const float mx = (float)(W - 1) / 2.f, my = (float)(H - 1) / 2.f;
+  gflow[(2 * n + 0) * plane + pix] = (gix * mx) / halfx;
+  gflow[(2 * n + 1) * plane + pix] = (giy * my) / halfy;
+}
+
 // PWC_WARP_CFG=<digit> selects a (channels per group, groups per thread) variant for
 // measurement: 0 = 4 channels per thread, XCD-grouped pixel blocks (default), 1 = 8, 2 = 2,
 // 3 = 4 without XCD grouping, 4 = 2 grouped, 5 = 8 grouped.
@@ -211,9 +422,57 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
   const size_t npix = (size_t)B * H * W;
   if (npix == 0) return hipSuccess;
   if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
+  const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
+  static const bool scatter = std::getenv("PWC_WARP_BWD") && std::getenv("PWC_WARP_BWD")[0] == '0';
+  if (!scatter) {
+    // grad_x tile shape (PWC_WARP_TILES=<variant> for measurement)
+    static const int tv = std::getenv("PWC_WARP_TILES") ? std::atoi(std::getenv("PWC_WARP_TILES")) : 0;
+    int th = 8, tw = 32;
+    if (C > 0) {
+      hipError_t e = hipSuccess;
+#define PWC_TILES(V, TW, CC)                                                                   \
+  if (tv == V) {                                                                               \
+    th = 256 / TW;                                                                             \
+    tw = TW;                                                                                   \
+    const int ntx = (W + TW - 1) / TW, nty = (H + th - 1) / th;                                \
+    hipLaunchKernelGGL((warp_bwd_gx_lists<TW, CC>),                                            \
+                       dim3((unsigned)(ntx * nty), (unsigned)B, (unsigned)((C + CC - 1) / CC)), \
+                       dim3(256), 0, stream, (const float*)flow, (const float*)gout,           \
+                       (float*)gx, C, H, W, halfx, halfy, ntx);                                \
+    e = hipGetLastError();                                                                     \
+  }
+      PWC_TILES(0, 32, 8)
+      PWC_TILES(1, 32, 4)
+      PWC_TILES(2, 32, 16)
+      PWC_TILES(3, 16, 8)
+      PWC_TILES(4, 64, 8)
+#undef PWC_TILES
+      if (e != hipSuccess) return e;
+    }
+    // channel groups for grids with few pixels (the coarse levels): ~64K threads or 16 groups
+    int ng = 1;
+    while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
+    if (const char* e = std::getenv("PWC_WARP_BWD_NG")) ng = std::atoi(e);
+    const int cpg = (C + ng - 1) / ng;
+    const unsigned blocks = (unsigned)((npix * ng + 255) / 256);
+#define PWC_FLOW(NGV)                                                                          \
+  if (ng == NGV) {                                                                             \
+    hipLaunchKernelGGL((warp_bwd_flow<8, NGV>), dim3(blocks), dim3(256), 0, stream,            \
+                       (const float*)x, (const float*)flow, (const float*)gout, (float*)gx,    \
+                       (float*)gflow, B, C, H, W, halfx, halfy, cpg, th, tw);                  \
+    return hipGetLastError();                                                                  \
+  }
+    PWC_FLOW(1)
+    PWC_FLOW(2)
+    PWC_FLOW(4)
+    PWC_FLOW(8)
+    PWC_FLOW(16)
+#undef PWC_FLOW
+    return hipErrorNotSupported;
+  }
+  // PWC_WARP_BWD=0: the scatter of ATen's kernel (global atomics into a zeroed grad_x)
   hipError_t e = hipMemsetAsync(gx, 0, sizeof(float) * npix * C, stream);
   if (e != hipSuccess) return e;
-  const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
   hipLaunchKernelGGL(warp_bwd_kernel<8>, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0,
                      stream, (const float*)x, (const float*)flow, (const float*)gout,
                      (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy);

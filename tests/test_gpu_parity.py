@@ -201,6 +201,23 @@ def test_warp_vs_oracle(shape):
     np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
 
 
+@pytest.mark.parametrize("scale", [0.0, 6.0, 25.0])
+def test_warp_backward_tiles_and_outliers(scale):
+    # grad_x of the LDS-binned kernel (tiles of 8x32, candidate margin 8) + the corners left
+    # to global atomics: zero flow, flows around the margin, and flows far beyond it; ragged
+    # tile edges (37 x 70) and a channel count that is not a multiple of the chunk (13)
+    from pwcnet_amd.ops import warp_backward
+    B, C, H, W = 2, 13, 37, 70
+    rng = np.random.default_rng(17)
+    x = _rand(rng, B, C, H, W)
+    f = (rng.standard_normal((B, 2, H, W)) * scale).astype(np.float32)
+    g = _rand(rng, B, C, H, W)
+    gx, gf = warp_backward(_t(x), _t(f), _t(g))
+    rx, rf = O.warp_backward(x, f, g)
+    np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
+
+
 def test_warp_fp16():
     from pwcnet_amd.ops import warp_forward
     rng = np.random.default_rng(5)

@@ -108,11 +108,11 @@ def main():
             med, mean = timeit(lambda s: corr_backward(s["x1"], s["x2"], go, 9, 1, 9, 1, 2),
                                sets, args.iters)
             print(json.dumps(dict(level=l, op="corr_bwd", shape=[B, C, h, w],
-                                  us=round(med, 2), min_us=round(mean, 2))))
+                                  us=round(med, 2), min_us=round(mean, 2), tag=args.tag)))
             gw = torch.randn(B, C, h, w, device=dev)
             med, mean = timeit(lambda s: warp_backward(s["x2"], s["fl"], gw), sets, args.iters)
             print(json.dumps(dict(level=l, op="warp_bwd", shape=[B, C, h, w],
-                                  us=round(med, 2), min_us=round(mean, 2))))
+                                  us=round(med, 2), min_us=round(mean, 2), tag=args.tag)))
 
 
 if __name__ == "__main__":
