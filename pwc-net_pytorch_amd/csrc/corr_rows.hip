@@ -143,10 +143,12 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) acc[ti][kk] = 0.f;
 
-  for (int cb = 0; cb < C; cb += g.ck) {
+  // the next chunk's loads are issued right after its staging slot frees up, so they are in
+  // flight during the current chunk's compute
+  f32x4 v1[ML1], v2[ML2];
+  auto issue = [&](int cb) {
     const int cn = min(g.ck, C - cb);
     const int so = (int)((uint32_t)cb * plane * 4u);
-    f32x4 v1[ML1], v2[ML2];
 #pragma unroll
     for (int j = 0; j < ML1; ++j)  // channels past C (last chunk) read zeros: range check
       v1[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -155,6 +157,10 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
     for (int j = 0; j < ML2; ++j)
       v2[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                             rs2, (int)(ch2[j] < cn ? vo2[j] : kOOB), so, 0));
+  };
+  issue(0);
+  for (int cb = 0; cb < C; cb += g.ck) {
+    const int cn = min(g.ck, C - cb);
     if (cb > 0) lds_barrier();  // the previous chunk's compute is done with the staging
 #pragma unroll
     for (int j = 0; j < ML1; ++j) {
@@ -168,6 +174,7 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
       *reinterpret_cast<f32x2*>(lds + ld2[j]) = f32x2{v2[j].x, v2[j].z};
       *reinterpret_cast<f32x2*>(lds + ld2[j] + g.Wf) = f32x2{v2[j].y, v2[j].w};
     }
+    if (cb + g.ck < C) issue(cb + g.ck);
     lds_barrier();
     if (active) {
       const float* pa = f1s + a_off;
