@@ -29,6 +29,10 @@
  *                             torch-0.4 semantics (bilinear, zeros, align_corners=True).
  *   pwc_warp_corr_forward  <- the two calls of one pyramid level, model.py:80 (warp) + :83
  *                             (corr), as one entry point (fused kernel where it applies).
+ *   pwc_upsample_warp_forward <- model.py:78 (F.upsample(flow, scale_factor=2,
+ *                             mode='bilinear') * 2, torch-0.4 align_corners=False) + :80
+ *                             (WarpingLayer) as one launch; pwc_flow_upsample_backward is the
+ *                             adjoint of model.py:78 (ATen upsample_bilinear2d_backward * 2).
  */
 #ifndef PWC_HOTPATH_H
 #define PWC_HOTPATH_H
@@ -51,7 +55,7 @@ extern "C" {
 #define PWC_DTYPE_BF16 2
 
 /* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
- * 4: fused warp -> correlation). */
+ * 4: fused warp -> correlation, 5: fused flow upsample -> warp). */
 PWC_API int pwc_abi_version(void);
 
 /* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
@@ -118,6 +122,18 @@ PWC_API int pwc_warp_forward(const void* x, const void* flow, void* out, int B, 
 PWC_API int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, void* grad_x,
                       void* grad_flow, int B, int C, int H, int W, int dtype, void* stream);
 
+/* model.py:78 + :80 in one launch: flow_up = bilinear x2 upsample of flow_coarse
+ * ([B][2][H/2][W/2], ATen upsample_bilinear2d with align_corners=False -- torch 0.4's default)
+ * times 2, then x2_warp = WarpingLayer(x2, flow_up) exactly as pwc_warp_forward on the stored
+ * flow_up.  H, W = the size of x2 (even).  flow_up ([B][2][H][W]) may be NULL (not needed);
+ * it is written otherwise (model.py:89/91 concatenates it). */
+PWC_API int pwc_upsample_warp_forward(const void* x2, const void* flow_coarse, void* flow_up,
+                                      void* x2_warp, int B, int C, int H, int W, int dtype,
+                                      void* stream);
+/* Adjoint of model.py:78: grad_flow_coarse ([B][2][H/2][W/2], written) from grad_flow_up
+ * ([B][2][H][W]); fixed-order gather, no atomics.  fp32. */
+PWC_API int pwc_flow_upsample_backward(const void* grad_flow_up, void* grad_flow_coarse, int B,
+                                       int H, int W, int dtype, void* stream);
 /* One pyramid level of model.py:80-83: x2_warp = WarpingLayer(x2, flow), then
  * out = Correlation(in1, x2_warp) exactly as pwc_warp_forward followed by pwc_corr_forward
  * (same values: x2_warp bit-identical, out within fp32 summation order).  x2_warp may be NULL

@@ -124,6 +124,62 @@ def warp_backward(x, flow, gout, dtype=np.float64):
     return gx, gf
 
 
+def _up2_taps(n_out, n_in):
+    """ATen upsample_bilinear2d source taps along one axis for a x2 upsample with
+    align_corners=False (area_pixel_compute_source_index: 0.5*(d+0.5)-0.5 clamped at 0;
+    i1 = i0 + (i0 < n_in-1); lambda1 = src - i0) -- torch 0.4's F.upsample default, used by
+    model.py:78."""
+    d = np.arange(n_out, dtype=np.float64)
+    src = np.maximum(0.5 * (d + 0.5) - 0.5, 0.0)
+    i0 = src.astype(np.int64)
+    i1 = i0 + (i0 < n_in - 1)
+    l1 = src - i0
+    return i0, i1, 1.0 - l1, l1
+
+
+def flow_upsample2(flow, dtype=np.float64):
+    """model.py:78: F.upsample(flow, scale_factor=2, mode='bilinear') * 2 (numpy)."""
+    f = _c(flow, dtype)
+    B, two, h, w = f.shape
+    y0, y1, ly0, ly1 = _up2_taps(2 * h, h)
+    x0, x1, lx0, lx1 = _up2_taps(2 * w, w)
+    ly0, ly1 = ly0[:, None], ly1[:, None]
+    top = lx0 * f[:, :, y0][:, :, :, x0] + lx1 * f[:, :, y0][:, :, :, x1]
+    bot = lx0 * f[:, :, y1][:, :, :, x0] + lx1 * f[:, :, y1][:, :, :, x1]
+    return ((ly0 * top + ly1 * bot) * 2).astype(dtype)
+
+
+def flow_upsample2_backward(grad_up, dtype=np.float64):
+    """Adjoint of flow_upsample2 (ATen upsample_bilinear2d_backward scatter, times 2)."""
+    g = _c(grad_up, dtype) * 2
+    B, two, H, W = g.shape
+    h, w = H // 2, W // 2
+    y0, y1, ly0, ly1 = _up2_taps(H, h)
+    x0, x1, lx0, lx1 = _up2_taps(W, w)
+    out = np.zeros((B, two, h, w), dtype)
+    for oy in range(H):
+        for (yy, wy) in ((y0[oy], ly0[oy]), (y1[oy], ly1[oy])):
+            for (xx, wx) in ((x0, lx0), (x1, lx1)):
+                np.add.at(out, (slice(None), slice(None), yy, xx), g[:, :, oy, :] * (wy * wx))
+    return out
+
+
+def upsample_warp_forward(x2, flow_coarse, dtype=np.float64):
+    """model.py:78 + :80: (x2_warp, flow_up)."""
+    fup = flow_upsample2(flow_coarse, dtype)
+    return warp_forward(x2, fup, dtype), fup
+
+
+def upsample_warp_backward(x2, flow_coarse, gout, gflow_up=None, dtype=np.float64):
+    """Gradients of upsample_warp_forward wrt x2 and the coarse flow for upstream gradients of
+    x2_warp (gout) and of flow_up (gflow_up, optional)."""
+    fup = flow_upsample2(flow_coarse, dtype)
+    gx, gf = warp_backward(x2, fup, gout, dtype)
+    if gflow_up is not None:
+        gf = gf + _c(gflow_up, dtype)
+    return gx, flow_upsample2_backward(gf, dtype)
+
+
 def cvl_offsets(sr):
     """(dy, dx) of each CostVolumeLayer channel, modules.py:58-72."""
     K = (2 * sr + 1) ** 2

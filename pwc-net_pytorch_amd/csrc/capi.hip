@@ -23,6 +23,10 @@ template <typename T>
 hipError_t warp_forward_t(const void*, const void*, void*, int, int, int, int, hipStream_t);
 hipError_t warp_backward_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                              int, hipStream_t);
+template <typename T>
+hipError_t upsample_warp_forward_t(const void*, const void*, void*, void*, int, int, int, int,
+                                   hipStream_t);
+hipError_t flow_up2_backward_f32(const void*, void*, int, int, int, hipStream_t);
 hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                               int, float, int, hipStream_t);
 }  // namespace pwc
@@ -88,7 +92,7 @@ int force_generic() {
 
 extern "C" {
 
-int pwc_abi_version(void) { return 4; }
+int pwc_abi_version(void) { return 5; }
 
 int pwc_time_next_corr(void* start_event, void* stop_event) {
   if ((start_event == nullptr) != (stop_event == nullptr))
@@ -346,6 +350,43 @@ int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, voi
                                                  W, (hipStream_t)stream));
 }
 
+int pwc_upsample_warp_forward(const void* x2, const void* flow_coarse, void* flow_up,
+                              void* x2_warp, int B, int C, int H, int W, int dtype,
+                              void* stream) {
+  const char* fn = "pwc_upsample_warp_forward";
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if ((H | W) & 1) return fail(fn, "H and W must be even (2x the coarse flow)");
+  if ((size_t)B * H * W && (!flow_coarse || (C && (!x2 || !x2_warp))))
+    return fail(fn, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case PWC_DTYPE_F32:
+      e = pwc::upsample_warp_forward_t<float>(x2, flow_coarse, flow_up, x2_warp, B, C, H, W, s);
+      break;
+    case PWC_DTYPE_F16:
+      e = pwc::upsample_warp_forward_t<__half>(x2, flow_coarse, flow_up, x2_warp, B, C, H, W, s);
+      break;
+    case PWC_DTYPE_BF16:
+      e = pwc::upsample_warp_forward_t<__hip_bfloat16>(x2, flow_coarse, flow_up, x2_warp, B, C,
+                                                       H, W, s);
+      break;
+    default:
+      return fail(fn, "unsupported dtype");
+  }
+  return check_launch(fn, e);
+}
+
+int pwc_flow_upsample_backward(const void* grad_flow_up, void* grad_flow_coarse, int B, int H,
+                               int W, int dtype, void* stream) {
+  const char* fn = "pwc_flow_upsample_backward";
+  if (!dims_ok(B, 2, H, W)) return fail(fn, "negative dimension");
+  if ((H | W) & 1) return fail(fn, "H and W must be even (2x the coarse flow)");
+  if (dtype != PWC_DTYPE_F32) return fail(fn, "backward is fp32 only");
+  if ((size_t)B * H * W && (!grad_flow_up || !grad_flow_coarse)) return fail(fn, "null buffer");
+  return check_launch(fn, pwc::flow_up2_backward_f32(grad_flow_up, grad_flow_coarse, B, H, W,
+                                                     (hipStream_t)stream));
+}
 
 // ---- fused warp -> correlation (model.py:80-83 as one call) ----
 // The fused kernel covers model.py:24's configuration (pad == md in {8, 9}, k 1, s1 1, s2 2)

@@ -56,15 +56,54 @@ __device__ __forceinline__ void warp_load(WarpGroup<T, CB>& g, const T* __restri
   }
 }
 
+// model.py:78: F.upsample(flow, scale_factor=2, mode='bilinear') * 2 under torch 0.4
+// (align_corners=False: ATen upsample_bilinear2d, area_pixel_compute_source_index with scale
+// 1/2, source index clamped at 0, right/bottom tap clamped to the last row/column), the same
+// fp32 operation order as ATen's kernel, then the exact *2.  `f` is one [h][w] plane.
+struct UpTap {
+  int i00, i01, i10, i11;
+  float l0y, l1y, l0x, l1x;
+};
+
+__device__ __forceinline__ UpTap up2_taps(int oy, int ox, int h, int w) {
+#pragma clang fp contract(off)
+  const float sy = fmaxf(0.5f * ((float)oy + 0.5f) - 0.5f, 0.f);
+  const float sx = fmaxf(0.5f * ((float)ox + 0.5f) - 0.5f, 0.f);
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int yp = y0 < h - 1 ? 1 : 0, xp = x0 < w - 1 ? 1 : 0;
+  UpTap t;
+  t.l1y = sy - (float)y0;
+  t.l0y = 1.f - t.l1y;
+  t.l1x = sx - (float)x0;
+  t.l0x = 1.f - t.l1x;
+  t.i00 = y0 * w + x0;
+  t.i01 = y0 * w + x0 + xp;
+  t.i10 = (y0 + yp) * w + x0;
+  t.i11 = (y0 + yp) * w + x0 + xp;
+  return t;
+}
+
+template <typename T>
+__device__ __forceinline__ float up2_value(const T* __restrict__ f, const UpTap& t) {
+#pragma clang fp contract(off)
+  const float v = t.l0y * (t.l0x * to_f32(f[t.i00]) + t.l1x * to_f32(f[t.i01])) +
+                  t.l1y * (t.l0x * to_f32(f[t.i10]) + t.l1x * to_f32(f[t.i11]));
+  return v * 2.f;
+}
+
 // One thread per output pixel; grid.y splits the channels into slices of NG groups of CB
 // channels, and a thread walks its slice's groups with the next group's gathers in flight
 // while the current one is blended and stored.  32-bit indexing (the launcher checks
 // B*C*H*W < 2^31).
-template <typename T, int CB, int NG, bool XCD>
+// UP: `flow` is the coarse [B][2][H/2][W/2] flow of the previous level, upsampled in registers
+// (model.py:78); the channel-slice-0 threads also write the upsampled flow to `flow_up` when
+// it is not null (model.py:89/91 concatenates it).
+template <typename T, int CB, int NG, bool XCD, bool UP = false>
 __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ flow,
                                                        T* __restrict__ out, int B, int C, int H,
-                                                       int W, float halfx, float halfy) {
+                                                       int W, float halfx, float halfy,
+                                                       T* __restrict__ flow_up = nullptr) {
   const unsigned plane = (unsigned)(H * W);
   // XCD: consecutive pixel blocks (which gather overlapping source rows) share an L2
   const unsigned bx = XCD ? (unsigned)xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -74,8 +113,31 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
   const unsigned pix = idx - n * plane;
   const int py = (int)(pix / (unsigned)W);
   const int px = (int)pix - py * W;
-  const float u = to_f32(flow[(2 * n + 0) * plane + pix]);
-  const float v = to_f32(flow[(2 * n + 1) * plane + pix]);
+  float u, v;
+  if constexpr (UP) {
+    const int h = H >> 1, w = W >> 1;
+    const UpTap tp = up2_taps(py, px, h, w);
+    const unsigned cplane = (unsigned)(h * w);
+    u = up2_value(flow + (2 * n + 0) * cplane, tp);
+    v = up2_value(flow + (2 * n + 1) * cplane, tp);
+    if constexpr (sizeof(T) == 4) {  // round like a stored fp32 flow, then use it
+      if (flow_up != nullptr && blockIdx.y == 0) {
+        flow_up[(2 * n + 0) * plane + pix] = u;
+        flow_up[(2 * n + 1) * plane + pix] = v;
+      }
+    } else {  // storage rounding first: the reference warps with the stored upsampled flow
+      const T ut = from_f32<T>(u), vt = from_f32<T>(v);
+      if (flow_up != nullptr && blockIdx.y == 0) {
+        flow_up[(2 * n + 0) * plane + pix] = ut;
+        flow_up[(2 * n + 1) * plane + pix] = vt;
+      }
+      u = to_f32(ut);
+      v = to_f32(vt);
+    }
+  } else {
+    u = to_f32(flow[(2 * n + 0) * plane + pix]);
+    v = to_f32(flow[(2 * n + 1) * plane + pix]);
+  }
   const float ix = src_coord(u, px, W, halfx);
   const float iy = src_coord(v, py, H, halfy);
   const Bilinear b = bilinear(ix, iy, H, W);
@@ -478,6 +540,72 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
                      (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy);
   return hipGetLastError();
 }
+
+// model.py:78 + :80 in one launch: x2_warp = warp(x2, up2(flow_coarse) * 2), flow_up written
+// when not null.  H and W are the fine (x2) sizes, both even.
+template <typename T>
+hipError_t upsample_warp_forward_t(const void* x, const void* flow_coarse, void* flow_up,
+                                   void* out, int B, int C, int H, int W, hipStream_t stream) {
+  const size_t npix = (size_t)B * H * W;
+  if (npix == 0) return hipSuccess;
+  if ((H | W) & 1) return hipErrorInvalidValue;
+  if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
+  const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
+  const unsigned gx = (unsigned)((npix + 255) / 256);
+  constexpr int CB = 4;
+  const unsigned gy = C > 0 ? (unsigned)((C + CB - 1) / CB) : 1u;
+  hipLaunchKernelGGL((warp_fwd_kernel<T, CB, 1, true, true>), dim3(gx, gy), dim3(256), 0, stream,
+                     (const T*)x, (const T*)flow_coarse, (T*)out, B, C, H, W, halfx, halfy,
+                     (T*)flow_up);
+  return hipGetLastError();
+}
+
+// Backward of model.py:78 (adjoint of up2 * 2, fp32): grad_coarse[n,ch,Y,X] = 2 * sum of
+// grad_up[n,ch,oy,ox] * tap weight over the fine pixels whose taps reach (Y,X) -- as a gather
+// over the fine rows/columns within 2 of (2Y, 2X) (each coarse pixel is tapped by at most 4
+// fine rows x 4 fine columns), fixed order: no atomics, deterministic.
+__global__ __launch_bounds__(256) void flow_up2_bwd_kernel(const float* __restrict__ gup,
+                                                           float* __restrict__ gc, int B,
+                                                           int H, int W) {
+  const int h = H >> 1, w = W >> 1;
+  const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= (unsigned)(B * 2 * h * w)) return;
+  const int X = (int)(idx % (unsigned)w);
+  const int Y = (int)((idx / (unsigned)w) % (unsigned)h);
+  const unsigned nc = idx / (unsigned)(h * w);
+  const float* g = gup + nc * (unsigned)(H * W);
+  const int tgt = Y * w + X;
+  float acc = 0.f;
+  for (int oy = max(0, 2 * Y - 2); oy <= min(H - 1, 2 * Y + 2); ++oy)
+    for (int ox = max(0, 2 * X - 2); ox <= min(W - 1, 2 * X + 2); ++ox) {
+      const UpTap t = up2_taps(oy, ox, h, w);
+      float wt = 0.f;  // ATen adds the four tap weights separately (taps may coincide)
+      if (t.i00 == tgt) wt += t.l0y * t.l0x;
+      if (t.i01 == tgt) wt += t.l0y * t.l1x;
+      if (t.i10 == tgt) wt += t.l1y * t.l0x;
+      if (t.i11 == tgt) wt += t.l1y * t.l1x;
+      if (wt != 0.f) acc += (2.f * g[oy * W + ox]) * wt;
+    }
+  gc[idx] = acc;
+}
+
+hipError_t flow_up2_backward_f32(const void* grad_up, void* grad_coarse, int B, int H, int W,
+                                 hipStream_t stream) {
+  const size_t n = (size_t)B * 2 * (H / 2) * (W / 2);
+  if (n == 0) return hipSuccess;
+  if ((H | W) & 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(flow_up2_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     (const float*)grad_up, (float*)grad_coarse, B, H, W);
+  return hipGetLastError();
+}
+
+template hipError_t upsample_warp_forward_t<float>(const void*, const void*, void*, void*, int,
+                                                   int, int, int, hipStream_t);
+template hipError_t upsample_warp_forward_t<__half>(const void*, const void*, void*, void*, int,
+                                                    int, int, int, hipStream_t);
+template hipError_t upsample_warp_forward_t<__hip_bfloat16>(const void*, const void*, void*,
+                                                            void*, int, int, int, int,
+                                                            hipStream_t);
 
 template hipError_t warp_forward_t<float>(const void*, const void*, void*, int, int, int, int,
                                           hipStream_t);

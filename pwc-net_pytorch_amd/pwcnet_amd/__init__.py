@@ -4,13 +4,15 @@ Drop-in surface (reference daigo0927/PWC-Net_pytorch):
   Correlation, CorrelationFunction   <- correlation_package (modules/functions correlation.py)
   WarpingLayer, CostVolumeLayer       <- modules.py:25-74
   WarpCorrelation, WarpCorrelationFunction <- model.py:80-83 (warp then correlation, fused)
+  UpsampleWarp, UpsampleWarpFunction  <- model.py:78 + :80 (flow upsample x2 then warp, fused)
   get_grid                            <- utils.py:3-8
 The kernels live in libpwc_hotpath.so (C ABI: include/pwc_hotpath.h); there is no CPU path.
 """
-from .layers import Correlation, CostVolumeLayer, WarpCorrelation, WarpingLayer, get_grid
-from .ops import (CorrelationFunction, CostVolumeFunction, WarpCorrelationFunction,
-                  WarpFunction)
+from .layers import (Correlation, CostVolumeLayer, UpsampleWarp, WarpCorrelation, WarpingLayer,
+                     get_grid)
+from .ops import (CorrelationFunction, CostVolumeFunction, UpsampleWarpFunction,
+                  WarpCorrelationFunction, WarpFunction)
 
 __all__ = ["Correlation", "CorrelationFunction", "CostVolumeLayer", "CostVolumeFunction",
            "WarpCorrelation", "WarpCorrelationFunction", "WarpingLayer", "WarpFunction",
-           "get_grid"]
+           "UpsampleWarp", "UpsampleWarpFunction", "get_grid"]

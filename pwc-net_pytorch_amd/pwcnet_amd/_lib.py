@@ -45,8 +45,10 @@ SYMBOLS = {
     "pwc_warp_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 5 + [_P]),
     "pwc_warp_corr_workspace_size": (_Z, [_I] * 11),
     "pwc_warp_corr_forward": (_I, [_P] * 5 + [_I] * 11 + [_P, _Z, _P]),
+    "pwc_upsample_warp_forward": (_I, [_P] * 4 + [_I] * 5 + [_P]),
+    "pwc_flow_upsample_backward": (_I, [_P, _P] + [_I] * 4 + [_P]),
 }
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lock = threading.Lock()
 _lib = None

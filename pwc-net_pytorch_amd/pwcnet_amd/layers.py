@@ -12,7 +12,8 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .ops import CorrelationFunction, CostVolumeFunction, WarpCorrelationFunction, WarpFunction
+from .ops import (CorrelationFunction, CostVolumeFunction, UpsampleWarpFunction,
+                  WarpCorrelationFunction, WarpFunction)
 
 
 class Correlation(nn.Module):
@@ -86,6 +87,22 @@ class WarpCorrelation(nn.Module):
         return WarpCorrelationFunction.apply(x1, x2, flow, self.pad_size, self.kernel_size,
                                              self.max_displacement, self.stride1, self.stride2,
                                              self.corr_multiply)
+
+
+class UpsampleWarp(nn.Module):
+    """model.py:78 + :80 in one call:
+
+        flow = F.upsample(flow, scale_factor=2, mode='bilinear') * 2     # model.py:78
+        x2_warp = self.warping_layer(x2, flow)                            # model.py:80
+    becomes
+        x2_warp, flow = self.upsample_warp(x2, flow)
+
+    torch 0.4's bilinear upsample (align_corners=False) and the WarpingLayer chain
+    (align_corners=True grid_sample); gradients flow to x2 and the coarse flow.
+    """
+
+    def forward(self, x2, flow_coarse):
+        return UpsampleWarpFunction.apply(x2, flow_coarse)
 
 
 class CostVolumeLayer(nn.Module):

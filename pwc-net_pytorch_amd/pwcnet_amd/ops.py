@@ -238,6 +238,70 @@ class WarpFunction(Function):
 
 
 # ---------------------------------------------------------------------------------------
+# model.py:78 + :80: flow upsample (x2, bilinear, * 2) then warp, fused
+# ---------------------------------------------------------------------------------------
+def upsample_warp_forward(x2, flow_coarse, emit_flow=True):
+    """(x2_warp, flow_up) with flow_up = F.upsample(flow_coarse, scale_factor=2,
+    mode='bilinear') * 2 (torch 0.4: align_corners=False) and x2_warp = WarpingLayer(x2,
+    flow_up): model.py:78 + :80 as one kernel launch.  ``emit_flow=False`` skips writing
+    flow_up (returned as None)."""
+    _check_inputs("UpsampleWarp", x2, flow_coarse)
+    B, C, H, W = x2.shape
+    if tuple(flow_coarse.shape) != (B, 2, H // 2, W // 2) or H % 2 or W % 2:
+        raise ValueError(f"UpsampleWarp: flow shape {tuple(flow_coarse.shape)} is not "
+                         f"{(B, 2, H // 2, W // 2)} (x2 {tuple(x2.shape)} must be 2x it)")
+    if flow_coarse.dtype != x2.dtype:
+        raise TypeError("UpsampleWarp: x2 and flow must share a dtype")
+    _i32(B, C, H, W, x2.numel(), B * 2 * H * W)
+    x2, flow_coarse = x2.contiguous(), flow_coarse.contiguous()
+    out = torch.empty_like(x2)
+    fup = torch.empty(B, 2, H, W, device=x2.device, dtype=x2.dtype) if emit_flow else None
+    if B * H * W == 0:
+        return out, fup
+    _lib.check(_lib.load().pwc_upsample_warp_forward(
+        _ptr(x2), _ptr(flow_coarse), _ptr(fup) if fup is not None else None, _ptr(out), B, C,
+        H, W, _lib.DTYPE_CODES[x2.dtype], _stream(x2.device)), "UpsampleWarp_forward")
+    return out, fup
+
+
+def flow_upsample_backward(grad_flow_up):
+    """Adjoint of model.py:78 (fp32): grad of the coarse flow from grad of flow_up."""
+    _check_inputs("UpsampleWarp backward", grad_flow_up, dtypes=(torch.float32,))
+    B, two, H, W = grad_flow_up.shape
+    if two != 2 or H % 2 or W % 2:
+        raise ValueError(f"flow upsample backward: bad shape {tuple(grad_flow_up.shape)}")
+    grad_flow_up = grad_flow_up.contiguous()
+    gc = torch.empty(B, 2, H // 2, W // 2, device=grad_flow_up.device, dtype=torch.float32)
+    if gc.numel() == 0:
+        return gc
+    _lib.check(_lib.load().pwc_flow_upsample_backward(_ptr(grad_flow_up), _ptr(gc), B, H, W, 0,
+                                                      _stream(grad_flow_up.device)),
+               "UpsampleWarp_backward")
+    return gc
+
+
+class UpsampleWarpFunction(Function):
+    @staticmethod
+    def forward(ctx, x2, flow_coarse):
+        x2, flow_coarse = x2.contiguous(), flow_coarse.contiguous()
+        with torch.cuda.device(x2.device):
+            out, fup = upsample_warp_forward(x2, flow_coarse)
+        ctx.save_for_backward(x2, fup)
+        return out, fup
+
+    @staticmethod
+    def backward(ctx, grad_out, grad_fup):
+        x2, fup = ctx.saved_tensors
+        with torch.cuda.device(x2.device):
+            gx2, gflow = (warp_backward(x2, fup, grad_out) if grad_out is not None
+                          else (None, torch.zeros_like(fup)))
+            if grad_fup is not None:
+                gflow = gflow + grad_fup
+            gcoarse = flow_upsample_backward(gflow)
+        return gx2, gcoarse
+
+
+# ---------------------------------------------------------------------------------------
 # one pyramid level of model.py:80-83: warp then correlation, fused
 # ---------------------------------------------------------------------------------------
 def warp_corr_forward(input1, x2, flow, pad_size, kernel_size, max_displacement, stride1,

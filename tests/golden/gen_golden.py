@@ -81,6 +81,32 @@ def _warp_case(M, name, seed, B, C, H, W, flow_std, zero_flow=False):
     print(name, tuple(out.shape))
 
 
+def _upwarp_case(M, name, seed, B, C, h, w, flow_std):
+    """model.py:78 (F.upsample(flow, scale_factor=2, mode='bilinear') * 2, called as the
+    reference calls it: torch 0.4's default is align_corners=False, as is modern torch's) then
+    model.py:80 (the reference WarpingLayer); gradients wrt x2 and the coarse flow for seeded
+    upstream gradients of x2_warp and of the upsampled flow (model.py:89/91 concatenates it)."""
+    g = torch.Generator().manual_seed(seed)
+    x2 = torch.randn(B, C, 2 * h, 2 * w, generator=g)
+    flow = torch.randn(B, 2, h, w, generator=g) * flow_std
+    args = types.SimpleNamespace(device="cpu")
+    xs = x2.clone().requires_grad_(True)
+    fs = flow.clone().requires_grad_(True)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        fup = F.upsample(fs, scale_factor=2, mode="bilinear") * 2
+    out = M.WarpingLayer(args)(xs, fup)
+    gout = torch.randn(out.shape, generator=g)
+    gfup = torch.randn(fup.shape, generator=g)
+    torch.autograd.backward([out, fup], [gout, gfup])
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), x2=x2.numpy(), flow=flow.numpy(),
+                        out=out.detach().numpy(), flow_up=fup.detach().numpy(),
+                        gout=gout.numpy(), gflow_up=gfup.numpy(), gx2=xs.grad.numpy(),
+                        gflow=fs.grad.numpy())
+    print(name, tuple(out.shape))
+
+
 def main():
     M = _load_reference()
     # CostVolumeLayer sr=4 ("Corr4" pin) and sr=8 ("Corr9" pin), SURVEY §8c shapes.
@@ -97,6 +123,9 @@ def main():
     _warp_case(M, "warp_b2c32_24x28", 12, 2, 32, 24, 28, 2.0)
     _warp_case(M, "warp_b1c16_9x31_far", 13, 1, 16, 9, 31, 12.0)
     _warp_case(M, "warp_b1c4_6x7_zero", 14, 1, 4, 6, 7, 0.0, zero_flow=True)
+    # flow upsample x2 (model.py:78) then warp (model.py:80): l0 -> l1 shape and a ragged one
+    _upwarp_case(M, "upwarp_b2c8_6x7", 21, 2, 8, 6, 7, 1.5)
+    _upwarp_case(M, "upwarp_b1c4_5x9_far", 22, 1, 4, 5, 9, 6.0)
 
 
 if __name__ == "__main__":

@@ -218,6 +218,58 @@ def test_warp_backward_tiles_and_outliers(scale):
     np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
 
 
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "upwarp_*.npz"))),
+                         ids=os.path.basename)
+def test_upsample_warp_vs_reference(path):
+    # model.py:78 + :80 as one launch (UpsampleWarp), reference fixtures incl. gradients
+    from pwcnet_amd import UpsampleWarp
+    z = np.load(path)
+    x2 = _t(z["x2"]).requires_grad_(True)
+    f = _t(z["flow"]).requires_grad_(True)
+    out, fup = UpsampleWarp()(x2, f)
+    torch.autograd.backward([out, fup], [_t(z["gout"]), _t(z["gflow_up"])])
+    np.testing.assert_allclose(_np(fup), z["flow_up"], rtol=1e-6, atol=1e-5)
+    np.testing.assert_allclose(_np(out), z["out"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_np(x2.grad), z["gx2"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(f.grad), z["gflow"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(8, 32, 96, 112), (2, 128, 12, 14), (1, 3, 10, 18)])
+def test_upsample_warp_vs_oracle(shape):
+    # fused == flow upsample then warp (oracle), at the l4 size and small/ragged ones; the
+    # warp of the stored flow_up is bit-identical to pwc_warp_forward on it
+    from pwcnet_amd.ops import flow_upsample_backward, upsample_warp_forward, warp_forward
+    B, C, H, W = shape
+    rng = np.random.default_rng(23)
+    x2 = _rand(rng, B, C, H, W)
+    f = (rng.standard_normal((B, 2, H // 2, W // 2)) * 2).astype(np.float32)
+    out, fup = upsample_warp_forward(_t(x2), _t(f))
+    np.testing.assert_allclose(_np(fup), O.flow_upsample2(f), rtol=1e-6, atol=1e-5)
+    # the warp is pinned on the flow it sampled with (the stored fp32 flow_up, as the reference
+    # stores it): an fp64 flow_up moves samples near integer coordinates by ~1 fp32 ulp
+    np.testing.assert_allclose(_np(out), O.warp_forward(x2, _np(fup)), rtol=1e-5, atol=1e-5)
+    assert torch.equal(out, warp_forward(_t(x2), fup))
+    out2, none = upsample_warp_forward(_t(x2), _t(f), emit_flow=False)
+    assert none is None and torch.equal(out, out2)
+    g = (rng.standard_normal((B, 2, H, W))).astype(np.float32)
+    np.testing.assert_allclose(_np(flow_upsample_backward(_t(g))), O.flow_upsample2_backward(g),
+                               rtol=1e-5, atol=1e-5)
+
+
+def test_upsample_warp_fp16_and_shape_checks():
+    from pwcnet_amd.ops import upsample_warp_forward
+    rng = np.random.default_rng(29)
+    x2 = _t(_rand(rng, 2, 16, 24, 28), torch.float16)
+    f = _t(rng.standard_normal((2, 2, 12, 14)) * 2, torch.float16)
+    out, fup = upsample_warp_forward(x2, f)
+    rfup = O.flow_upsample2(_np(f))
+    np.testing.assert_allclose(_np(fup), rfup, rtol=2e-3, atol=2e-3)
+    # fp16 warps with the STORED (fp16-rounded) upsampled flow, like the reference would
+    np.testing.assert_allclose(_np(out), O.warp_forward(_np(x2), _np(fup)), rtol=2e-3, atol=5e-3)
+    with pytest.raises(ValueError):
+        upsample_warp_forward(_t(_rand(rng, 1, 4, 11, 14)), _t(_rand(rng, 1, 2, 5, 7)))
+
+
 def test_warp_fp16():
     from pwcnet_amd.ops import warp_forward
     rng = np.random.default_rng(5)

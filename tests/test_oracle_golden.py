@@ -82,3 +82,28 @@ def test_corr_shape_math():
     # k=3 -> kr=1, br=3: Ho = ceil((20+6-6)/2) = 10, Wo = ceil((30+6-6)/2) = 15
     assert O.corr_output_shape(20, 30, 3, 3, 2, 2, 1) == (25, 10, 15)
     assert O.corr_output_shape(21, 31, 3, 3, 2, 2, 1) == (25, 11, 16)  # ceil(10.5)
+
+
+UPWARP = sorted(glob.glob(os.path.join(GOLDEN, "upwarp_*.npz")))
+
+
+@pytest.mark.parametrize("path", UPWARP, ids=os.path.basename)
+def test_upsample_warp_vs_reference(path):
+    # model.py:78 (F.upsample x2, align_corners=False, * 2) + :80 (WarpingLayer), reference run
+    z = np.load(path)
+    out, fup = O.upsample_warp_forward(z["x2"], z["flow"])
+    np.testing.assert_allclose(fup, z["flow_up"], rtol=1e-6, atol=1e-5)
+    np.testing.assert_allclose(out, z["out"], rtol=1e-5, atol=1e-5)
+    gx, gf = O.upsample_warp_backward(z["x2"], z["flow"], z["gout"], z["gflow_up"])
+    np.testing.assert_allclose(gx, z["gx2"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(gf, z["gflow"], rtol=1e-4, atol=1e-4)
+
+
+def test_flow_upsample_adjoint():
+    # <up(f), g> == <f, up^T(g)>: the backward is the exact adjoint of the forward
+    rng = np.random.default_rng(3)
+    f = rng.standard_normal((2, 2, 5, 7))
+    g = rng.standard_normal((2, 2, 10, 14))
+    lhs = float((O.flow_upsample2(f) * g).sum())
+    rhs = float((f * O.flow_upsample2_backward(g)).sum())
+    assert abs(lhs - rhs) <= 1e-9 * max(1.0, abs(lhs))

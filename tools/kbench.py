@@ -103,6 +103,20 @@ def main():
                                   band=os.environ.get("PWC_BAND_CFG", ""), us=round(med, 2),
                                   min_us=round(mean, 2), gbs=round(fb / (med * 1e-6) / 1e9, 1),
                                   tag=args.tag)))
+        if "upwarp" in ops and h % 2 == 0 and w % 2 == 0:
+            # model.py:78 + :80: fused flow upsample -> warp (flow_up emitted) against the
+            # unfused ATen upsample * 2 followed by the warp kernel
+            from pwcnet_amd.ops import upsample_warp_forward
+            import torch.nn.functional as F
+            for s in sets:
+                s["fc"] = s["fl"][:, :, ::2, ::2].contiguous()
+            med, mean = timeit(lambda s: upsample_warp_forward(s["x2"], s["fc"]), sets,
+                               args.iters)
+            med2, _ = timeit(lambda s: warp_forward(s["x2"], F.interpolate(
+                s["fc"], scale_factor=2, mode="bilinear", align_corners=False) * 2), sets,
+                args.iters)
+            print(json.dumps(dict(level=l, op="upsample_warp", shape=[B, C, h, w],
+                                  us=round(med, 2), unfused_us=round(med2, 2), tag=args.tag)))
         if args.backward and dt == torch.float32:
             go = torch.randn(B, 81, h, w, device=dev)
             med, mean = timeit(lambda s: corr_backward(s["x1"], s["x2"], go, 9, 1, 9, 1, 2),
