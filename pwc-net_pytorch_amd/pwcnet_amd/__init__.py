@@ -6,6 +6,7 @@ Drop-in surface (reference daigo0927/PWC-Net_pytorch):
   WarpCorrelation, WarpCorrelationFunction <- model.py:80-83 (warp then correlation, fused)
   UpsampleWarp, UpsampleWarpFunction  <- model.py:78 + :80 (flow upsample x2 then warp, fused)
   get_grid                            <- utils.py:3-8
+  flow_io.load_flow/save_flow/vis_flow <- flow_utils.py (.flo I/O + colour coding, numpy)
 The kernels live in libpwc_hotpath.so (C ABI: include/pwc_hotpath.h); there is no CPU path.
 """
 from .layers import (Correlation, CostVolumeLayer, UpsampleWarp, WarpCorrelation, WarpingLayer,
