@@ -19,6 +19,8 @@
  *                             correlation_cuda.h:1-8) -> Correlation_forward_cuda_kernel
  *                             (correlation_cuda_kernel.h:5-38, .cu:296-369).  No rInput1/
  *                             rInput2 scratch: the NHWC transpose (cu:10-32) is not needed.
+ *   pwc_corr_forward_into  <- model.py:83-84 (corr, optional leaky_relu_) feeding the cat of
+ *                             model.py:89/91, as one call writing the cat buffer's slice
  *   pwc_corr_backward      <- Correlation_backward_cuda (correlation_cuda.c:95-180,
  *                             correlation_cuda.h:10-17) -> Correlation_backward_cuda_kernel
  *                             (correlation_cuda_kernel.h:40-88, .cu:371-473)
@@ -55,7 +57,7 @@ extern "C" {
 #define PWC_DTYPE_BF16 2
 
 /* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
- * 4: fused warp -> correlation, 5: fused flow upsample -> warp). */
+ * 4: fused warp -> correlation, 5: fused flow upsample -> warp, corr into a slice). */
 PWC_API int pwc_abi_version(void);
 
 /* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
@@ -91,6 +93,23 @@ PWC_API int pwc_corr_forward_ws(const void* in1, const void* in2, void* out, int
                         int stride1, int stride2, int corr_multiply, int dtype,
                         void* workspace, size_t workspace_bytes, void* stream);
 
+/* model.py:83-84 + :89/91: the correlation written straight into a caller's buffer slice --
+ * image n's OC x Ho x Wo block starts at out + n * out_image_stride elements (e.g. the corr
+ * channels of the cat([x1, corr, flow], 1) buffer: out = buf + C*H*W, stride (C+OC+2)*H*W) --
+ * with every value passed through leaky_relu(negative_slope) (model.py:84's in-place
+ * F.leaky_relu_ when args.corr_activation, slope 0.01; 1.0 = no activation, bit-identical to
+ * pwc_corr_forward).  For model.py:24's configuration in fp32 the correlation kernels write
+ * the slice themselves; other configurations compute the dense volume in `workspace` (at least
+ * pwc_corr_forward_into_workspace_size() bytes; may be NULL when not needed) and copy it. */
+PWC_API size_t pwc_corr_forward_into_workspace_size(int B, int C, int H, int W, int pad_size,
+                                                    int kernel_size, int max_displacement,
+                                                    int stride1, int stride2, int dtype);
+PWC_API int pwc_corr_forward_into(const void* in1, const void* in2, void* out,
+                                  long long out_image_stride, float negative_slope, int B, int C,
+                                  int H, int W, int pad_size, int kernel_size,
+                                  int max_displacement, int stride1, int stride2,
+                                  int corr_multiply, int dtype, void* workspace,
+                                  size_t workspace_bytes, void* stream);
 /* grad_in1/grad_in2 ([B][C][H][W]) from grad_out ([B][OC][Ho][Wo]) exactly as
  * correlation_cuda_kernel.cu:108-290.  Requires stride1 == 1 (the reference backward is
  * undefined otherwise: it indexes gradInput with the strided coordinate).  Every element of

@@ -3,6 +3,7 @@
 // Argument checks mirror what the reference enforced or silently assumed
 // (correlation_package/functions/correlation.py:17-18 contiguity asserts are done by the
 // Python layer; correlation_cuda.c:20-42 shape math and fills; cu:361-368 launch check).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -32,6 +33,29 @@ hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void
 }  // namespace pwc
 
 namespace pwc {
+// output epilogue of the next correlation launch of this thread (pwc_corr_forward_into)
+thread_local OutEpi g_epi = {0, 1.f};
+OutEpi current_epi() { return g_epi; }
+
+struct EpiScope {
+  EpiScope(long long ostride, float slope) { g_epi = OutEpi{ostride, slope}; }
+  ~EpiScope() { g_epi = OutEpi{0, 1.f}; }
+};
+
+// dst[n * ostride + i] = leaky(src[n * vol + i]) -- the fallback of pwc_corr_forward_into for
+// configurations whose kernels write dense volumes only
+template <typename T>
+__global__ __launch_bounds__(256) void copy_strided_act(const T* __restrict__ src,
+                                                        T* __restrict__ dst, size_t vol,
+                                                        long long ostride, float slope,
+                                                        size_t total) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * 256) {
+    const size_t n = i / vol, e = i - n * vol;
+    dst[n * (size_t)ostride + e] = from_f32<T>(epi_act(to_f32(src[i]), slope));
+  }
+}
+
 thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
 void take_launch_events(hipEvent_t* start, hipEvent_t* stop) {
   *start = g_ev_start;
@@ -154,6 +178,78 @@ static int corr_forward_impl(const char* fn, const void* in1, const void* in2, v
       return fail(fn, "unsupported dtype");
   }
   return check_launch(fn, e);
+}
+
+size_t pwc_corr_forward_into_workspace_size(int B, int C, int H, int W, int pad_size,
+                                            int kernel_size, int max_displacement, int stride1,
+                                            int stride2, int dtype) {
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W) ||
+      !corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo) ||
+      Ho <= 0 || Wo <= 0)
+    return 0;
+  const size_t esz = dtype == PWC_DTYPE_F32 ? 4 : 2;
+  return (size_t)B * OC * Ho * Wo * esz;
+}
+
+int pwc_corr_forward_into(const void* in1, const void* in2, void* out,
+                          long long out_image_stride, float negative_slope, int B, int C, int H,
+                          int W, int pad_size, int kernel_size, int max_displacement,
+                          int stride1, int stride2, int corr_multiply, int dtype,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  (void)corr_multiply;  // ignored, as in the reference (cu)
+  const char* fn = "pwc_corr_forward_into";
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (!corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo))
+    return fail(fn, "invalid correlation parameters");
+  if (Ho <= 0 || Wo <= 0) return fail(fn, "empty correlation output");
+  const long long vol = (long long)OC * Ho * Wo;
+  if (B > 1 && out_image_stride < vol) return fail(fn, "out_image_stride < OC*Ho*Wo");
+  if (!(negative_slope == negative_slope)) return fail(fn, "negative_slope is NaN");
+  if (B == 0) return check_launch(fn, hipSuccess);
+  if (!in1 || !in2 || !out) return fail(fn, "null buffer");
+  const long long ostride = out_image_stride > 0 ? out_image_stride : vol;
+  const float divisor = (float)(kernel_size * kernel_size * C);  // cu:65 nelems
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype != PWC_DTYPE_F32 && dtype != PWC_DTYPE_F16 && dtype != PWC_DTYPE_BF16)
+    return fail(fn, "unsupported dtype");
+  hipError_t e = hipErrorNotSupported;
+  if (dtype == PWC_DTYPE_F32 && force_generic() == 0) {  // kernels that write the slice directly
+    pwc::EpiScope scope(ostride == vol ? 0 : ostride, negative_slope);
+    e = pwc::corr_forward_t<float>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size, kernel_size,
+                                   max_displacement, stride1, stride2, pwc::kRaster, divisor,
+                                   nullptr, s, 0);
+  }
+  if (e != hipErrorNotSupported) return check_launch(fn, e);
+  // dense volume in the workspace, then one strided copy applying the activation
+  const size_t esz = dtype == PWC_DTYPE_F32 ? 4 : 2;
+  if (!workspace || workspace_bytes < (size_t)B * vol * esz)
+    return fail(fn, "workspace smaller than pwc_corr_forward_into_workspace_size()");
+  if (!corr_forward_impl(fn, in1, in2, workspace, B, C, H, W, pad_size, kernel_size,
+                         max_displacement, stride1, stride2, dtype, nullptr, 0, stream))
+    return 0;
+  const size_t total = (size_t)B * vol;
+  const unsigned blocks = (unsigned)std::min<size_t>((total + 255) / 256, 65536);
+  switch (dtype) {
+    case PWC_DTYPE_F32:
+      hipLaunchKernelGGL(pwc::copy_strided_act<float>, dim3(blocks), dim3(256), 0, s,
+                         (const float*)workspace, (float*)out, (size_t)vol, ostride,
+                         negative_slope, total);
+      break;
+    case PWC_DTYPE_F16:
+      hipLaunchKernelGGL(pwc::copy_strided_act<__half>, dim3(blocks), dim3(256), 0, s,
+                         (const __half*)workspace, (__half*)out, (size_t)vol, ostride,
+                         negative_slope, total);
+      break;
+    default:
+      hipLaunchKernelGGL(pwc::copy_strided_act<__hip_bfloat16>, dim3(blocks), dim3(256), 0, s,
+                         (const __hip_bfloat16*)workspace, (__hip_bfloat16*)out, (size_t)vol,
+                         ostride, negative_slope, total);
+  }
+  return check_launch(fn, hipGetLastError());
 }
 
 size_t pwc_corr_workspace_size(int B, int C, int H, int W, int pad_size, int kernel_size,

@@ -544,6 +544,9 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
   const int D = 2 * dr + 1;
   const int max_splits = workspace ? corr_max_splits(B, D * D, Ho, Wo) : 1;
   if (max_splits <= 1) workspace = nullptr;
+  // a strided / activated output (pwc_corr_forward_into) is written by the band, row-band,
+  // parity-tile and ring kernels only; every other path declines before launching
+  const bool epi_def = epi_is_default(current_epi());
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && layout == kRaster &&
       s2 == 2 && pad == md && (md == 8 || md == 9) &&
       (band_mode() == 2 || (band_mode() == 1 && (H + 1) / 2 <= 6))) {
@@ -567,7 +570,8 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
     }
     // the smallest levels (l0, l1: a few hundred pixels, unaligned rows): whole parity halves
     // per workgroup, channel slices over the workspace (corr_small.hip)
-    if (dr == 4 && s2 == 2 && 9 * ((Ho + 1) / 2) * ((Wo + 7) / 8) <= 256 && !pt_disabled()) {
+    if (dr == 4 && s2 == 2 && 9 * ((Ho + 1) / 2) * ((Wo + 7) / 8) <= 256 && !pt_disabled() &&
+        epi_def) {
       const hipError_t e = corr_forward_small_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad,
                                                   dr, s2, layout, divisor, max_splits,
                                                   workspace, stream);
@@ -577,7 +581,7 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
     // in-workgroup channel groups (corr_grp.hip); unaligned rows (W % 4 != 0, the smallest
     // pyramid levels) measured faster on the channel-split path below.
     const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
-    if (tiles < 256 && W % 4 == 0 && (md - pad) % 4 == 0 && !grp_disabled()) {
+    if (tiles < 256 && W % 4 == 0 && (md - pad) % 4 == 0 && !grp_disabled() && epi_def) {
       const hipError_t e = corr_forward_grp_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad,
                                                 dr, s2, layout, divisor, stream);
       if (e != hipErrorNotSupported) return e;
@@ -587,6 +591,7 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
                                                stream);
     if (e != hipErrorNotSupported) return e;
   }
+  if (!epi_def) return hipErrorNotSupported;
   if (force_generic != 1 && k == 1 && s1 == 1 && dr == 4) {
     const int off = md - pad;
     if (s2 == 2)

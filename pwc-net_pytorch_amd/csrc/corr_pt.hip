@@ -199,7 +199,7 @@ template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
     int C, int H, int W, int Ho, int Wo, int off, int layout, float divisor, float inv_divisor,
-    int n_tr, int n_tx) {
+    int n_tr, int n_tx, OutEpi epi) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
 
   // tile order: image-major, then parity, tile row, tile column; the XCD remap keeps an
@@ -345,7 +345,8 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
   const int OC = G::D * G::D;
   const bool pow2 = inv_divisor != 0.f;
   const bool has_hi = ox + 4 < Wo;
-  float* obase = out + (((size_t)n * OC) * Ho + oy) * Wo + ox;
+  float* obase = out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * OC * Ho * Wo) +
+                 (size_t)oy * Wo + ox;
   auto emit = [&](int v, f32x4 q) {  // v = 2*ti + h
     const int ti = v >> 1, h = v & 1;
     if (!st_ok || (h && !has_hi)) return;
@@ -354,6 +355,8 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_pt(
       q *= inv_divisor;
     else
       q /= divisor;
+    q = f32x4{epi_act(q.x, epi.slope), epi_act(q.y, epi.slope), epi_act(q.z, epi.slope),
+              epi_act(q.w, epi.slope)};
     st_out4(obase + (size_t)oc * Ho * Wo + 4 * h, q);
   };
   if constexpr (G::K == 1) {
@@ -410,7 +413,7 @@ static hipError_t launch_pt(const void* in1, const void* in2, void* out, int B, 
   take_launch_events(&ev0, &ev1);
   hipExtLaunchKernelGGL((corr_fwd_pt<G>), dim3((unsigned)nblk), dim3(G::THREADS), G::LDS_BYTES,
                         stream, ev0, ev1, 0, (const float*)in1, (const float*)in2, (float*)out,
-                        C, H, W, Ho, Wo, off, layout, divisor, inv, n_tr, n_tx);
+                        C, H, W, Ho, Wo, off, layout, divisor, inv, n_tr, n_tx, current_epi());
   return hipGetLastError();
 }
 

@@ -177,7 +177,7 @@ template <class G>
 __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
     int C, int H, int W, int Ho, int Wo, int off, int layout, float divisor, float inv_divisor,
-    int n_ty, int n_tx, int cps, float* __restrict__ partial
+    int n_ty, int n_tx, int cps, float* __restrict__ partial, OutEpi epi
 #ifdef PWC_RING_CENSUS
     , unsigned* census
 #endif
@@ -342,10 +342,11 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     return;
   }
   const bool pow2 = inv_divisor != 0.f;
+  float* oimg = out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * OC * Ho * Wo);
 #pragma unroll
   for (int ti = 0; ti < G::D; ++ti) {
     const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
-    float* orow = out + (((size_t)n * OC + oc) * Ho + oy) * Wo;
+    float* orow = oimg + ((size_t)oc * Ho + oy) * Wo;
     st_f32x4 v;
     if (pow2)
       v = st_f32x4{acc[ti][0] * inv_divisor, acc[ti][1] * inv_divisor,
@@ -353,6 +354,8 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
     else
       v = st_f32x4{acc[ti][0] / divisor, acc[ti][1] / divisor, acc[ti][2] / divisor,
                    acc[ti][3] / divisor};
+    v = st_f32x4{epi_act(v.x, epi.slope), epi_act(v.y, epi.slope), epi_act(v.z, epi.slope),
+                 epi_act(v.w, epi.slope)};
     st_out4(orow + ox, v);
   }
 }
@@ -947,6 +950,8 @@ static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B
   if (nsplit < 1) nsplit = 1;
   const int cps = ((nchunks + nsplit - 1) / nsplit) * G::CC;
   nsplit = (C + cps - 1) / cps;
+  const OutEpi epi = current_epi();
+  if (nsplit > 1 && !epi_is_default(epi)) return hipErrorNotSupported;  // dense partials only
   // exact reciprocal when the divisor is a power of two (then x * inv == x / divisor)
   int ex;
   const float m = std::frexp(divisor, &ex);
@@ -958,7 +963,7 @@ static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B
   hipExtLaunchKernelGGL((corr_fwd_ring<G>), dim3((unsigned)nblk, (unsigned)nsplit),
                         dim3(G::THREADS), G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1,
                         (const float*)in2, (float*)out, C, H, W, Ho, Wo, off, layout, divisor,
-                        inv, n_ty, n_tx, cps, (float*)partial
+                        inv, n_ty, n_tx, cps, (float*)partial, epi
 #ifdef PWC_RING_CENSUS
                         , g_census
 #endif
@@ -1046,7 +1051,9 @@ hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, in
   if ((size_t)C * H * W * 4 >= 0x7ffffff0ull) return hipErrorNotSupported;
   const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
   const int ns = partial ? corr_pick_splits(tiles, (C + 3) / 4, max_splits) : 1;
-  switch (ring_cfg()) {
+  const int rc = ring_cfg();
+  if (!epi_is_default(current_epi()) && rc >= 5 && rc <= 12) return hipErrorNotSupported;
+  switch (rc) {
     case 0: return launch_ring<RingA>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
     case 1: return launch_ring<RingB>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
     case 3: return launch_ring<RingD>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
                                                        const float* __restrict__ f2,
                                                        float* __restrict__ out, int C, int H,
                                                        int W, float divisor, float inv_divisor,
-                                                       Geo g) {
+                                                       Geo g, OutEpi epi) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NR2 = R + 8;
   const int t = threadIdx.x;
@@ -231,7 +231,10 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
       v4 *= inv_divisor;
     else
       v4 = f32x4{v4.x / divisor, v4.y / divisor, v4.z / divisor, v4.w / divisor};
-    st_out4(out + ((size_t)(n * (D * D) + tj * D + ti) * H + (2 * row + p)) * W + 4 * m, v4);
+    v4 = f32x4{epi_act(v4.x, epi.slope), epi_act(v4.y, epi.slope), epi_act(v4.z, epi.slope),
+               epi_act(v4.w, epi.slope)};
+    const size_t ib = epi.ostride ? (size_t)n * epi.ostride : (size_t)n * (D * D) * H * W;
+    st_out4(out + ib + ((size_t)(tj * D + ti) * H + (2 * row + p)) * W + 4 * m, v4);
   }
 }
 
@@ -304,7 +307,7 @@ hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, in
     }                                                                                         \
     hipExtLaunchKernelGGL((corr_fwd_rows<RR, NT, M1, M2>), dim3((unsigned)g.units), dim3(NT), \
                           lds, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,     \
-                          (float*)out, C, H, W, divisor, inv, g);                             \
+                          (float*)out, C, H, W, divisor, inv, g, current_epi());              \
     return hipGetLastError();                                                                 \
   }
   PWC_ROWS(3, 2, 7)   // l4 at CK 16: 1.75 / 6.4 loads per thread per chunk

@@ -112,6 +112,23 @@ __device__ __forceinline__ void st_out1(float* p, float v) {
 #endif
 }
 
+// Output epilogue of the model-path correlation kernels: image n's
+// 81-channel block starts at out + n * ostride elements (ostride 0: dense, n * 81 * H * W) --
+// so a kernel can write straight into the corr slice of model.py:89/91's cat([x1, corr, flow])
+// buffer -- and every value goes through leaky_relu with `slope` (model.py:84's in-place
+// F.leaky_relu_, slope 0.01; slope 1 is the identity, bit for bit).
+struct OutEpi {
+  long long ostride;
+  float slope;
+};
+
+__device__ __forceinline__ float epi_act(float v, float slope) { return v > 0.f ? v : v * slope; }
+
+// Host side: the descriptor the next launch of this thread uses (capi.hip sets it around a
+// pwc_corr_forward_into call; default dense / identity).
+OutEpi current_epi();
+inline bool epi_is_default(const OutEpi& e) { return e.ostride == 0 && e.slope == 1.f; }
+
 // XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle must
 // be bijective"): consecutive logical tiles land on the same XCD (and L2), so neighbouring
 // tiles that re-read each other's halo rows hit the same L2.  Pure speed choice.

@@ -87,7 +87,7 @@ template <int R, int T, bool WARP>
 __global__ __launch_bounds__(NT, 1) void warp_corr_band(
     const float* __restrict__ f1, const float* __restrict__ x2, const float* __restrict__ flow,
     float* __restrict__ x2w, float* __restrict__ out, int C, int H, int W, float divisor,
-    float inv_divisor, float halfx, float halfy, Geo g) {
+    float inv_divisor, float halfx, float halfy, Geo g, OutEpi epi) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NR2 = R + T - 1;  // f2 parity rows staged
   BAND_MARK(0);
@@ -339,7 +339,9 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(
     for (; gg < g.G; ++gg) s0 += sp[gg * gstride];
     float sum = (s0 + s1) + (s2 + s3);
     sum = inv_divisor != 0.f ? sum * inv_divisor : sum / divisor;
-    st_out1(out + ((unsigned)(n * (D * D) + tj * D + ti) * H + (2 * row + p)) * W + x, sum);
+    const size_t ib = epi.ostride ? (size_t)n * epi.ostride : (size_t)n * (D * D) * H * W;
+    st_out1(out + ib + ((size_t)(tj * D + ti) * H + (2 * row + p)) * W + x,
+            epi_act(sum, epi.slope));
   }
   if (g.abl & 256) {
     __syncthreads();
@@ -380,7 +382,7 @@ static hipError_t launch(const float* f1, const float* x2, const float* flow, fl
   take_launch_events(&ev0, &ev1);
   hipExtLaunchKernelGGL((warp_corr_band<R, T, WARP>), dim3((unsigned)(g.units * ntg)), dim3(NT),
                         lds, stream, ev0, ev1, 0, f1, x2, flow, x2w, out, C, H, W, divisor, inv,
-                        halfx, halfy, g);
+                        halfx, halfy, g, current_epi());
   return hipGetLastError();
 }
 

@@ -47,6 +47,9 @@ SYMBOLS = {
     "pwc_warp_corr_forward": (_I, [_P] * 5 + [_I] * 11 + [_P, _Z, _P]),
     "pwc_upsample_warp_forward": (_I, [_P] * 4 + [_I] * 5 + [_P]),
     "pwc_flow_upsample_backward": (_I, [_P, _P] + [_I] * 4 + [_P]),
+    "pwc_corr_forward_into_workspace_size": (_Z, [_I] * 10),
+    "pwc_corr_forward_into": (_I, [_P, _P, _P, ctypes.c_longlong, ctypes.c_float] + [_I] * 11
+                              + [_P, _Z, _P]),
 }
 ABI_VERSION = 5
 

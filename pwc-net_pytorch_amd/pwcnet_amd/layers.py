@@ -12,7 +12,8 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .ops import (CorrelationFunction, CostVolumeFunction, UpsampleWarpFunction,
+from .ops import (CorrelationCatFunction, CorrelationFunction, CostVolumeFunction,
+                  UpsampleWarpFunction,
                   WarpCorrelationFunction, WarpFunction)
 
 
@@ -87,6 +88,29 @@ class WarpCorrelation(nn.Module):
         return WarpCorrelationFunction.apply(x1, x2, flow, self.pad_size, self.kernel_size,
                                              self.max_displacement, self.stride1, self.stride2,
                                              self.corr_multiply)
+
+
+class CorrelationCat(nn.Module):
+    """model.py:83-91 in one call:
+
+        corr = self.corr(x1, x2_warp)                                  # model.py:83
+        if args.corr_activation: F.leaky_relu_(corr)                   # model.py:84
+        ... torch.cat([x1, corr, flow], dim = 1) ...                   # model.py:89/91
+    becomes
+        inp = self.corr_cat(x1, x2_warp, flow)
+
+    The correlation kernels write straight into the concatenated buffer's corr channels
+    (with the leaky_relu fused when ``corr_activation``); ctor as ``Correlation``."""
+
+    def __init__(self, pad_size=9, kernel_size=1, max_displacement=9, stride1=1, stride2=2,
+                 corr_multiply=1, corr_activation=False, negative_slope=0.01):
+        super().__init__()
+        self.params = (pad_size, kernel_size, max_displacement, stride1, stride2)
+        self.negative_slope = negative_slope if corr_activation else None
+
+    def forward(self, x1, x2_warp, flow):
+        return CorrelationCatFunction.apply(x1, x2_warp, flow, *self.params,
+                                            self.negative_slope)
 
 
 class UpsampleWarp(nn.Module):

@@ -105,6 +105,71 @@ def corr_backward(input1, input2, grad_output, pad_size, kernel_size, max_displa
     return g1, g2
 
 
+def corr_forward_into(input1, input2, out, pad_size, kernel_size, max_displacement, stride1,
+                      stride2, corr_multiply=1, negative_slope=None):
+    """Correlation written into ``out`` -- a (B, OC, Ho, Wo) view whose images may sit at any
+    stride (e.g. ``buf[:, C:C+OC]`` of model.py:89/91's cat buffer) -- optionally through
+    leaky_relu (model.py:84).  fp32 model.py:24 correlations are written by the kernels."""
+    _check_inputs("Correlation into", input1, input2, out)
+    B, C, H, W = input1.shape
+    OC, Ho, Wo = _lib.corr_output_shape(H, W, pad_size, kernel_size, max_displacement, stride1,
+                                        stride2)
+    if tuple(out.shape) != (B, OC, Ho, Wo) or out.dtype != input1.dtype:
+        raise ValueError(f"Correlation into: out {tuple(out.shape)} {out.dtype} != "
+                         f"{(B, OC, Ho, Wo)} {input1.dtype}")
+    if out.stride()[1:] != (Ho * Wo, Wo, 1) or (B > 1 and out.stride(0) < OC * Ho * Wo):
+        raise ValueError("Correlation into: each image's block of `out` must be contiguous")
+    _i32(B, C, H, W, input1.numel())
+    input1, input2 = input1.contiguous(), input2.contiguous()
+    lib = _lib.load()
+    args = (B, C, H, W, pad_size, kernel_size, max_displacement, stride1, stride2)
+    nbytes = lib.pwc_corr_forward_into_workspace_size(*args, _lib.DTYPE_CODES[input1.dtype])
+    ws, wptr = _workspace(nbytes, input1.device)  # used only by the dense-then-copy fallback
+    slope = 1.0 if negative_slope is None else float(negative_slope)
+    _lib.check(lib.pwc_corr_forward_into(
+        _ptr(input1), _ptr(input2), _ptr(out), out.stride(0), slope, *args, corr_multiply,
+        _lib.DTYPE_CODES[input1.dtype], wptr, nbytes, _stream(input1.device)),
+        "Correlation_forward_into")
+    return out
+
+
+class CorrelationCatFunction(Function):
+    """cat([x1, act(corr(x1, x2_warp)), flow], 1) of model.py:83-91 with the correlation written
+    into the cat buffer by the kernels (no separate volume, no copy of it)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2_warp, flow, pad_size, kernel_size, max_displacement, stride1,
+                stride2, negative_slope):
+        x1, x2_warp, flow = x1.contiguous(), x2_warp.contiguous(), flow.contiguous()
+        B, C, H, W = x1.shape
+        OC, Ho, Wo = _lib.corr_output_shape(H, W, pad_size, kernel_size, max_displacement,
+                                            stride1, stride2)
+        if (Ho, Wo) != (H, W) or tuple(flow.shape[2:]) != (H, W):
+            raise ValueError("CorrelationCat: the correlation must keep the feature size "
+                             "(pad_size == max_displacement, kernel_size 1, stride1 1)")
+        buf = torch.empty(B, C + OC + flow.shape[1], H, W, device=x1.device, dtype=x1.dtype)
+        buf[:, :C].copy_(x1)
+        buf[:, C + OC:].copy_(flow)
+        with torch.cuda.device(x1.device):
+            corr_forward_into(x1, x2_warp, buf[:, C:C + OC], pad_size, kernel_size,
+                              max_displacement, stride1, stride2, 1, negative_slope)
+        ctx.params = (pad_size, kernel_size, max_displacement, stride1, stride2, negative_slope,
+                      C, OC)
+        ctx.save_for_backward(x1, x2_warp, buf)
+        return buf
+
+    @staticmethod
+    def backward(ctx, g):
+        x1, x2_warp, buf = ctx.saved_tensors
+        pad, k, md, s1, s2, slope, C, OC = ctx.params
+        gcorr = g[:, C:C + OC]
+        if slope is not None:  # in-place leaky_relu_: derivative from the result's sign
+            gcorr = torch.where(buf[:, C:C + OC] > 0, gcorr, gcorr * slope)
+        with torch.cuda.device(x1.device):
+            g1, g2 = corr_backward(x1, x2_warp, gcorr.contiguous(), pad, k, md, s1, s2)
+        return (g[:, :C] + g1, g2, g[:, C + OC:], None, None, None, None, None, None)
+
+
 class CorrelationFunction(Function):
     """Drop-in for correlation_package/functions/correlation.py:7-56 (same signature and
     defaults, same contiguity asserts, backward returns (g1, g2) + (None,) * 6)."""

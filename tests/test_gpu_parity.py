@@ -270,6 +270,63 @@ def test_upsample_warp_fp16_and_shape_checks():
         upsample_warp_forward(_t(_rand(rng, 1, 4, 11, 14)), _t(_rand(rng, 1, 2, 5, 7)))
 
 
+@pytest.mark.parametrize("shape", [(2, 192, 6, 7), (2, 128, 12, 14), (2, 96, 24, 28),
+                                   (2, 64, 48, 56), (2, 32, 96, 112)])
+@pytest.mark.parametrize("slope", [None, 0.01])
+def test_corr_forward_into_cat_slice(shape, slope):
+    # model.py:83-91: the kernels write the corr channels of the cat buffer (with the fused
+    # leaky_relu_); values equal corr_forward (+ F.leaky_relu) bit for bit, and nothing
+    # outside the slice is touched
+    from pwcnet_amd.ops import corr_forward, corr_forward_into
+    B, C, H, W = shape
+    rng = np.random.default_rng(31)
+    x1, x2 = _t(_rand(rng, B, C, H, W)), _t(_rand(rng, B, C, H, W))
+    buf = torch.full((B, C + 83, H, W), 7.25, device=DEV)
+    corr_forward_into(x1, x2, buf[:, C:C + 81], 9, 1, 9, 1, 2, negative_slope=slope)
+    ref = corr_forward(x1, x2, 9, 1, 9, 1, 2)
+    if slope is not None:
+        ref = torch.nn.functional.leaky_relu(ref, slope)
+    assert torch.equal(buf[:, C:C + 81], ref)
+    assert bool((buf[:, :C] == 7.25).all()) and bool((buf[:, C + 81:] == 7.25).all())
+
+
+@pytest.mark.parametrize("case", [("fp16", 9, 2), ("fp32", 4, 1)])
+def test_corr_forward_into_fallback(case):
+    # configurations without slice-writing kernels: dense volume + strided copy
+    from pwcnet_amd.ops import corr_forward, corr_forward_into
+    dt, md, s2 = case
+    dtype = torch.float16 if dt == "fp16" else torch.float32
+    B, C, H, W = 2, 16, 12, 14
+    rng = np.random.default_rng(37)
+    x1, x2 = _t(_rand(rng, B, C, H, W), dtype), _t(_rand(rng, B, C, H, W), dtype)
+    buf = torch.full((B, C + 83, H, W), -3.0, device=DEV, dtype=dtype)
+    corr_forward_into(x1, x2, buf[:, C:C + 81], md, 1, md, 1, s2, negative_slope=0.1)
+    ref = torch.nn.functional.leaky_relu(corr_forward(x1, x2, md, 1, md, 1, s2).float(), 0.1)
+    np.testing.assert_allclose(_np(buf[:, C:C + 81]), _np(ref), rtol=2e-3, atol=1e-4)
+    assert bool((buf[:, :C] == -3.0).all()) and bool((buf[:, C + 81:] == -3.0).all())
+
+
+@pytest.mark.parametrize("act", [False, True])
+def test_correlation_cat_autograd(act):
+    from pwcnet_amd import Correlation, CorrelationCat
+    B, C, H, W = 2, 32, 24, 28
+    rng = np.random.default_rng(41)
+    a, b, f = _rand(rng, B, C, H, W), _rand(rng, B, C, H, W), _rand(rng, B, 2, H, W)
+    g = _t(_rand(rng, B, C + 83, H, W))
+    x1, x2, fl = (_t(v).requires_grad_(True) for v in (a, b, f))
+    out = CorrelationCat(corr_activation=act)(x1, x2, fl)
+    out.backward(g)
+    y1, y2, yf = (_t(v).requires_grad_(True) for v in (a, b, f))
+    corr = Correlation(9, 1, 9, 1, 2)(y1, y2)
+    if act:
+        corr = torch.nn.functional.leaky_relu(corr, 0.01)
+    ref = torch.cat([y1, corr, yf], 1)
+    ref.backward(g)
+    assert torch.equal(out.detach(), ref.detach())
+    for u, v in ((x1, y1), (x2, y2), (fl, yf)):
+        np.testing.assert_allclose(_np(u.grad), _np(v.grad), rtol=1e-5, atol=1e-6)
+
+
 def test_warp_fp16():
     from pwcnet_amd.ops import warp_forward
     rng = np.random.default_rng(5)
