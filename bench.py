@@ -127,7 +127,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--fused-levels", default=os.environ.get("PWC_BENCH_FUSED", "0,1"),
                     help="levels run as one fused warp->correlation launch (WarpCorrelation)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01e_l4corr_pmc.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01f_l4corr_pmc.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
