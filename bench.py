@@ -10,14 +10,30 @@ the first image's features.  Per GPU the batch is 8 pairs (config 2); with --gpu
 rank processes its own 8 pairs (config 3: 64 pairs over 8 GPUs), no collective on the data
 path ("scaling": "weak").
 
-Timed region: every step replays its own hipGraph holding the whole pass (warp + correlation
-at l0..l4 on one stream); the l4 correlation -- the dominant kernel, priced for the roofline --
-is captured through hipExtLaunchKernel with that step's start/stop events, so its duration is
-measured live in every timed step.  Inputs rotate over enough buffer sets (> 2x the 256 MiB
-Infinity Cache) that each step reads them from HBM.
+Launch: ``bench.py --gpus N`` with N > 1 and no torch.distributed environment starts N ranks
+itself (a ``torch.distributed.run`` child, before this process touches the GPU) and exits
+with its status; under an outer launcher ``--gpus`` must equal WORLD_SIZE.  At N > 1 rank 0
+broadcasts the Net harness's weights (pwcnet_amd/net.py; SURVEY §8e's startup broadcast) and
+every rank checks it received them.
 
-cpu_baseline: the fp32 CPU port of the same path (oracle/pwc_oracle.c, OpenMP) on the same
-workload, rank 0 at N=1 only, timed for ~10 s.
+Timed region: every step replays the hipGraph of its buffer set (warp + correlation at l0..l3
+and the l4 warp) and then launches the l4 correlation -- the dominant kernel, priced for the
+roofline -- through the C ABI with hipExtLaunchKernel start/stop events (pwc_time_next_corr),
+so that kernel's duration is measured live in every timed step on the stream it runs on.
+Inputs rotate over enough buffer sets (> 2x the 256 MiB Infinity Cache) that each step reads
+them from HBM.  After timing, a replay self-check re-runs one step with every output poisoned
+(NaN) and compares all five levels bit for bit with a fresh eager computation, and a shard
+check compares per-pair checksums of every rank with rank 0's recomputation of the whole
+global batch (all_gather) -- a step that skipped a kernel, or a rank that computed the wrong
+pairs, fails the run.
+
+cpu_baseline (rank 0, N=1 only): the reference's pure-PyTorch CPU path restated
+(oracle/torch_ref.py: WarpingLayer = grid_sample(align_corners=True) + CostVolumeLayer, the
+reference's CPU correlation) over the same pyramid shapes, on every host thread torch is
+given; ``cpu_baseline_port`` is the fp32 C port of the GPU semantics (Corr9), labelled.
+
+``--device cpu`` (gloo) is a launcher rehearsal for the tests: the same launcher, sharding,
+broadcast and shard check with a torch-CPU stand-in for the per-shard op (not the product).
 """
 from __future__ import annotations
 
@@ -25,6 +41,9 @@ import argparse
 import ctypes
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -44,6 +63,7 @@ SEARCH_RANGE = 4
 CORR_ARGS = dict(pad_size=2 * SEARCH_RANGE + 1, kernel_size=1,
                  max_displacement=2 * SEARCH_RANGE + 1, stride1=1, stride2=2)  # model.py:24
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+PAIR_SEED = 20240601   # synthetic pair g of the checked set is seeded PAIR_SEED + g
 
 
 def level_shapes(H, W):
@@ -61,58 +81,10 @@ def corr_bytes_per_pair(C, h, w, elem=4):
     return (2 * C * h * w + 81 * h * w) * elem
 
 
-def make_set(shapes, B, dev, dtype, gen):
-    s = []
-    for (C, h, w) in shapes:
-        x1 = torch.randn(B, C, h, w, device=dev, generator=gen).to(dtype)
-        x2 = torch.randn(B, C, h, w, device=dev, generator=gen).to(dtype)
-        flow = (torch.randn(B, 2, h, w, device=dev, generator=gen) * 2.0).to(dtype)
-        corr = torch.empty(B, 81, h, w, device=dev, dtype=dtype)
-        s.append(dict(x1=x1, x2=x2, flow=flow, corr=corr))
-    return s
-
-
-def cpu_baseline(shapes, B, seconds, threads):
-    from oracle import oracle as O
-    rng = np.random.default_rng(0)
-    data = []
-    for (C, h, w) in shapes:
-        data.append((rng.standard_normal((B, C, h, w)).astype(np.float32),
-                     rng.standard_normal((B, C, h, w)).astype(np.float32),
-                     (rng.standard_normal((B, 2, h, w)) * 2).astype(np.float32)))
-    O.set_num_threads(threads, np.float32)
-    used = O.num_threads(np.float32)
-
-    def one():
-        for x1, x2, fl in data:
-            w = O.warp_forward(x2, fl, dtype=np.float32)
-            O.corr_forward(x1, w, 9, 1, 9, 1, 2, dtype=np.float32)
-
-    one()  # warm-up
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        one()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or reps >= 2000:
-            break
-    return dict(value=reps * B / el, unit="image-pairs/s", cores=used, kind="port",
-                sample=f"{reps} reps x {B} pairs of the same workload (warp + Corr9 at l0-l4, "
-                       f"384x448 pyramid shapes), fp32 oracle/pwc_oracle.c with {used} OpenMP "
-                       f"threads, {el:.1f} s")
-
-
-def load_pmc_traffic(path):
-    """HBM bytes per launch of the l4 correlation from a committed rocprofv3 PMC summary."""
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
-
-
-def main():
+# ---------------------------------------------------------------------------------------
+# launcher
+# ---------------------------------------------------------------------------------------
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -125,123 +97,428 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--fused-levels", default=os.environ.get("PWC_BENCH_FUSED", "0,1"),
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = launcher rehearsal over gloo with a torch-CPU stand-in op")
+    ap.add_argument("--fused-levels", default="0,1",
                     help="levels run as one fused warp->correlation launch (WarpCorrelation)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01f_l4corr_pmc.json"))
-    args = ap.parse_args()
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_l4corr_pmc.json"))
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(args, argv) -> int:
+    """Start args.gpus ranks of this script (one process per GPU) under torch.distributed.run
+    and return its exit status.  Called before anything touches the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------------------
+# synthetic inputs
+# ---------------------------------------------------------------------------------------
+def pair_inputs(g, shapes, dtype):
+    """Level inputs (x1, x2, flow) of global pair g, from a CPU generator seeded by g (any rank
+    can regenerate any pair)."""
+    gen = torch.Generator().manual_seed(PAIR_SEED + g)
+    out = []
+    for (C, h, w) in shapes:
+        x1 = torch.randn(C, h, w, generator=gen)
+        x2 = torch.randn(C, h, w, generator=gen)
+        fl = torch.randn(2, h, w, generator=gen) * 2.0
+        out.append((x1.to(dtype), x2.to(dtype), fl.to(dtype)))
+    return out
+
+
+def checked_set(pairs, shapes, dev, dtype):
+    """Buffer set of the given global pairs (seeded inputs)."""
+    per = [pair_inputs(g, shapes, dtype) for g in pairs]
+    s = []
+    for l, (C, h, w) in enumerate(shapes):
+        s.append(dict(x1=torch.stack([p[l][0] for p in per]).to(dev),
+                      x2=torch.stack([p[l][1] for p in per]).to(dev),
+                      flow=torch.stack([p[l][2] for p in per]).to(dev),
+                      corr=torch.empty(len(pairs), 81, h, w, device=dev, dtype=dtype)))
+    return s
+
+
+def random_set(shapes, B, dev, dtype, gen):
+    s = []
+    for (C, h, w) in shapes:
+        s.append(dict(x1=torch.randn(B, C, h, w, device=dev, generator=gen).to(dtype),
+                      x2=torch.randn(B, C, h, w, device=dev, generator=gen).to(dtype),
+                      flow=(torch.randn(B, 2, h, w, device=dev, generator=gen) * 2.0).to(dtype),
+                      corr=torch.empty(B, 81, h, w, device=dev, dtype=dtype)))
+    return s
+
+
+# ---------------------------------------------------------------------------------------
+# the per-shard pass: HIP path (product) or the CPU rehearsal stand-in
+# ---------------------------------------------------------------------------------------
+class HipPass:
+    """warp + Correlation(model.py:24) at l0..l4 through pwcnet_amd (C ABI); the l4
+    correlation is a direct, pre-bound C-ABI call so it can carry the timing events."""
+
+    def __init__(self, dev, dtype, fused):
+        from pwcnet_amd import _lib
+        from pwcnet_amd.ops import corr_forward, warp_corr_forward, warp_forward
+        self._lib = _lib
+        self.lib = _lib.load()  # raises if the HIP library is missing: there is no fallback
+        self.warp_forward, self.corr_forward = warp_forward, corr_forward
+        self.warp_corr_forward = warp_corr_forward
+        self.dev, self.dtype, self.fused = dev, dtype, fused
+        self.stream = torch.cuda.current_stream(dev)
+        self.sp = ctypes.c_void_p(self.stream.cuda_stream)
+        self.dcode = _lib.DTYPE_CODES[dtype]
+
+    def pre(self, s):
+        """l0..l3 (warp + corr; fused levels as one WarpCorrelation launch that also emits
+        x2_warp) and the l4 warp; the l4 warped features land in s[-1]["x2w"]."""
+        for l, lv in enumerate(s[:-1]):
+            if l in self.fused:
+                lv["corr"], lv["x2w"] = self.warp_corr_forward(lv["x1"], lv["x2"], lv["flow"],
+                                                               **CORR_ARGS)
+            else:
+                lv["x2w"] = self.warp_forward(lv["x2"], lv["flow"])
+                lv["corr"] = self.corr_forward(lv["x1"], lv["x2w"], **CORR_ARGS)
+        s[-1]["x2w"] = self.warp_forward(s[-1]["x2"], s[-1]["flow"])
+
+    def corr_l4(self, s, events=None):
+        lv = s[-1]
+        B, C, h, w = lv["x1"].shape
+        if events is not None:
+            self._lib.check(self.lib.pwc_time_next_corr(ctypes.c_void_p(events[0].cuda_event),
+                                                        ctypes.c_void_p(events[1].cuda_event)),
+                            "bench")
+        ret = self.lib.pwc_corr_forward(ctypes.c_void_p(lv["x1"].data_ptr()),
+                                        ctypes.c_void_p(lv["x2w"].data_ptr()),
+                                        ctypes.c_void_p(lv["corr"].data_ptr()), B, C, h, w,
+                                        9, 1, 9, 1, 2, 1, self.dcode, self.sp)
+        if ret != 1:
+            self._lib.check(ret, "bench corr_l4")
+
+    def full(self, s):
+        self.pre(s)
+        self.corr_l4(s)
+
+    def fresh(self, s):
+        """Unfused eager recomputation of every level (the self-check's reference)."""
+        out = []
+        for lv in s:
+            x2w = self.warp_forward(lv["x2"], lv["flow"])
+            out.append(self.corr_forward(lv["x1"], x2w, **CORR_ARGS))
+        return out
+
+
+class CpuStandinPass:
+    """--device cpu launcher rehearsal only: the same pass on the torch-CPU restatement."""
+
+    def __init__(self):
+        from oracle import torch_ref
+        self.T = torch_ref
+
+    def full(self, s):
+        for lv in s:
+            lv["x2w"] = self.T.warp(lv["x2"], lv["flow"])
+            lv["corr"] = self.T.correlation(lv["x1"], lv["x2w"], **CORR_ARGS)
+
+    def fresh(self, s):
+        return [self.T.correlation(lv["x1"], self.T.warp(lv["x2"], lv["flow"]), **CORR_ARGS)
+                for lv in s]
+
+
+def _same(a, b):
+    """Bit-identical, NaN == NaN (a 1-pixel level divides by W - 1 = 0, as the reference)."""
+    return a.shape == b.shape and torch.allclose(a, b, rtol=0.0, atol=0.0, equal_nan=True)
+
+
+def _diff(a, b):
+    """max |a - b| / (1 + |b|) with NaN positions required to match (inf if they do not, or if
+    the shapes differ).  The fused levels (one WarpCorrelation launch) may sum in a different
+    order than the unfused recomputation; a skipped kernel leaves the NaN poison."""
+    if a.shape != b.shape:
+        return float("inf")
+    na, nb = torch.isnan(a), torch.isnan(b)
+    if not torch.equal(na, nb):
+        return float("inf")
+    if na.all():
+        return 0.0
+    d = ((a - b).abs() / (1 + b.abs()))[~na]
+    return float(d.max()) if d.numel() else 0.0
+
+
+def pair_checksums(s):
+    """(pairs, levels, 2) float64: sum and sum of squares of each pair's volume per level."""
+    cols = []
+    for lv in s:
+        c = lv["corr"].double().flatten(1)
+        cols.append(torch.stack([c.sum(1), (c * c).sum(1)], 1))
+    return torch.stack(cols, 1)
+
+
+def shard_check(pass_, shapes, B, world, rank, dev, dtype):
+    """Every rank computes its own pairs [rank*B, rank*B + B) of the checked set; rank 0
+    gathers the per-pair checksums and compares them with its own computation of all
+    world*B pairs (same batch composition -> bit-identical arithmetic)."""
+    mine = list(range(rank * B, rank * B + B))
+    s = checked_set(mine, shapes, dev, dtype)
+    pass_.full(s)
+    cs = pair_checksums(s)
+    if world > 1:
+        parts = [torch.empty_like(cs) for _ in range(world)]
+        dist.all_gather(parts, cs)
+    else:
+        parts = [cs]
+    if rank != 0:
+        return None
+    bad = []
+    for r in range(world):
+        ref = checked_set(list(range(r * B, r * B + B)), shapes, dev, dtype)
+        pass_.full(ref)
+        exp = pair_checksums(ref)
+        if not _same(exp, parts[r]):
+            bad.append(r)
+    return {"pairs": world * B, "ranks": world, "ok": not bad, "bad_ranks": bad}
+
+
+def broadcast_weights(dev):
+    """one broadcast of the Net harness's weights from rank 0; every rank checks
+    it holds rank 0's parameters afterwards (checksums all_gathered)."""
+    from pwcnet_amd.net import Net, NetArgs
+    from pwcnet_amd.shard import broadcast_module
+    torch.manual_seed(1000 + dist.get_rank())  # ranks start with different weights
+    net = Net(NetArgs()).to(dev)
+    nbytes = sum(p.numel() * p.element_size() for p in net.parameters())
+    t0 = time.perf_counter()
+    broadcast_module(net, src=0)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    cs = torch.stack([p.detach().double().sum() for p in net.parameters()]).to(dev)
+    parts = [torch.empty_like(cs) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, cs)
+    ok = all(torch.equal(p, parts[0]) for p in parts)
+    return {"bytes": nbytes, "seconds": round(el, 4), "ok": ok}
+
+
+# ---------------------------------------------------------------------------------------
+# CPU baselines (rank 0, N = 1)
+# ---------------------------------------------------------------------------------------
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline_torch(shapes, B, seconds):
+    """The reference's pure-PyTorch CPU path (WarpingLayer + CostVolumeLayer at l0..l4,
+    oracle/torch_ref.py) on B pairs of the same pyramid shapes, every thread torch has."""
+    from oracle import torch_ref as T
+    gen = torch.Generator().manual_seed(0)
+    data = [(torch.randn(B, C, h, w, generator=gen), torch.randn(B, C, h, w, generator=gen),
+             torch.randn(B, 2, h, w, generator=gen) * 2) for (C, h, w) in shapes]
+
+    def one():
+        with torch.no_grad():
+            for x1, x2, fl in data:
+                T.cost_volume(x1, T.warp(x2, fl), SEARCH_RANGE)
+
+    one()  # warm-up
+    times = []
+    t_end = time.perf_counter() + seconds
+    while True:
+        t0 = time.perf_counter()
+        one()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() >= t_end or len(times) >= 200:
+            break
+    med = float(np.median(times))
+    thr = torch.get_num_threads()
+    return dict(value=round(B / med, 2), unit="image-pairs/s", cores=thr, kind="port",
+                cpu=cpu_model(), host_cpus=os.cpu_count(),
+                affinity_cpus=len(os.sched_getaffinity(0)),
+                sample=f"median of {len(times)} passes x {B} pairs, {sum(times):.1f} s: the "
+                       "reference's pure-PyTorch CPU path (WarpingLayer = grid_sample("
+                       "align_corners=True) + CostVolumeLayer(sr=4), modules.py:31-74) at "
+                       f"l0-l4 of 384x448, fp32, torch.get_num_threads()={thr}")
+
+
+def cpu_baseline_port(shapes, B, seconds, threads):
+    """fp32 C port of the GPU semantics (warp + Corr9, oracle/pwc_oracle.c, OpenMP)."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(0)
+    data = [(rng.standard_normal((B, C, h, w)).astype(np.float32),
+             rng.standard_normal((B, C, h, w)).astype(np.float32),
+             (rng.standard_normal((B, 2, h, w)) * 2).astype(np.float32)) for (C, h, w) in shapes]
+    O.set_num_threads(threads, np.float32)
+    used = O.num_threads(np.float32)
+
+    def one():
+        for x1, x2, fl in data:
+            O.corr_forward(x1, O.warp_forward(x2, fl, dtype=np.float32), 9, 1, 9, 1, 2,
+                           dtype=np.float32)
+
+    one()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 2000:
+            break
+    return dict(value=round(reps * B / el, 2), unit="image-pairs/s", cores=used, kind="port",
+                sample=f"{reps} reps x {B} pairs (warp + Corr9 at l0-l4, 384x448 shapes), fp32 "
+                       f"C port oracle/pwc_oracle.c, {used} OpenMP threads, {el:.1f} s")
+
+
+def load_pmc_traffic(path):
+    """HBM bytes per launch of the l4 correlation from a committed rocprofv3 PMC summary."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    except (OSError, ValueError):
+        return None, None
+
+
+# ---------------------------------------------------------------------------------------
+# main
+# ---------------------------------------------------------------------------------------
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return spawn_ranks(args, argv)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
 
-    from pwcnet_amd import _lib
-    from pwcnet_amd.ops import warp_forward, corr_forward, warp_corr_forward
+    cpu = args.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        if not torch.cuda.is_available():
+            print("bench.py: no HIP device (use --device cpu for the launcher rehearsal)",
+                  file=sys.stderr)
+            return 3
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
     from pwcnet_amd.shard import max_over_ranks
-    lib = _lib.load()
 
     dtype = torch.float32 if args.dtype == "fp32" else torch.float16
     esz = 4 if dtype == torch.float32 else 2
     B = args.batch
     shapes = level_shapes(args.height, args.width)
-    per_set = sum((2 * C * h * w + 2 * h * w + 81 * h * w + C * h * w) * B * esz
-                  for C, h, w in shapes)
-    nsets = args.sets or max(2, int(np.ceil(2 * 256 * 2 ** 20 / per_set)))
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    sets = [make_set(shapes, B, dev, dtype, gen) for _ in range(nsets)]
-    stream = torch.cuda.current_stream(dev)
-
-    # l4 correlation: direct C-ABI launch with pre-bound arguments
-    C4, h4, w4 = shapes[-1]
-    dcode = _lib.DTYPE_CODES[dtype]
-    sp = ctypes.c_void_p(stream.cuda_stream)
-
-    def corr_l4(s, x2w):
-        ret = lib.pwc_corr_forward(ctypes.c_void_p(s[-1]["x1"].data_ptr()),
-                                   ctypes.c_void_p(x2w.data_ptr()),
-                                   ctypes.c_void_p(s[-1]["corr"].data_ptr()), B, C4, h4, w4,
-                                   9, 1, 9, 1, 2, 1, dcode, sp)
-        if ret != 1:
-            _lib.check(ret, "bench corr_l4")
-
     fused = {int(v) for v in args.fused_levels.split(",") if v.strip()}
+    bcast = broadcast_weights(dev) if world > 1 else None
 
-    def pre(s):
-        """levels l0..l3 (warp + corr; fused levels as one WarpCorrelation launch that also
-        emits x2_warp) and the l4 warp; returns the l4 warped features."""
-        for l, lv in enumerate(s[:-1]):
-            if l in fused:
-                lv["corr"], lv["x2w"] = warp_corr_forward(lv["x1"], lv["x2"], lv["flow"],
-                                                          **CORR_ARGS)
-            else:
-                lv["x2w"] = warp_forward(lv["x2"], lv["flow"])
-                lv["corr"] = corr_forward(lv["x1"], lv["x2w"], **CORR_ARGS)
-        return warp_forward(s[-1]["x2"], s[-1]["flow"])
-
-    # warm the kernels (first-call attribute setup) before any capture
-    for s in sets:
-        corr_l4(s, pre(s))
-    torch.cuda.synchronize(dev)
-
-    # One hipGraph per timed step (levels l0..l4, warp + correlation, on one stream), each
-    # replayed once in the timed region; the l4 correlation inside it is launched through
-    # hipExtLaunchKernel with that step's start/stop events (pwc_time_next_corr), so its
-    # duration is measured live in every timed step.  (Warm-up replays the same graphs first.)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    for a, b in evs:  # materialise the hipEvent_t handles (torch creates them lazily)
-        a.record(stream)
-        b.record(stream)
-    torch.cuda.synchronize(dev)
-
-    def one_pass(s, ev=None):
-        w = pre(s)
-        if ev is not None:
-            _lib.check(lib.pwc_time_next_corr(ctypes.c_void_p(ev[0].cuda_event),
-                                               ctypes.c_void_p(ev[1].cuda_event)), "bench")
-        corr_l4(s, w)
+    if cpu:
+        pass_ = CpuStandinPass()
+        sets = [checked_set(list(range(rank * B, rank * B + B)), shapes, dev, dtype)]
+        nsets = 1
+    else:
+        pass_ = HipPass(dev, dtype, fused)
+        per_set = sum((2 * C * h * w + 2 * h * w + 81 * h * w + C * h * w) * B * esz
+                      for C, h, w in shapes)
+        nsets = args.sets or max(2, int(np.ceil(2 * 256 * 2 ** 20 / per_set)))
+        gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+        sets = [random_set(shapes, B, dev, dtype, gen) for _ in range(nsets)]
 
     graphs = []
-    if not args.no_graph:
-        pool = torch.cuda.graph_pool_handle()
-        for i in range(args.steps):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                one_pass(sets[i % nsets], evs[i])
-            graphs.append(g)
+    if not cpu:
+        for s in sets:  # first calls (kernel attributes) outside any capture
+            pass_.full(s)
+        torch.cuda.synchronize(dev)
+        if not args.no_graph:
+            # one hipGraph per buffer set: warp + corr at l0..l3 and the l4 warp.  The l4
+            # correlation stays an eager launch after the replay so its start/stop events are
+            # real per-step measurements (an event-armed launch must never be captured).
+            pool = torch.cuda.graph_pool_handle()
+            for s in sets:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    pass_.pre(s)
+                graphs.append(g)
+            torch.cuda.synchronize(dev)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        for a, b in evs:  # materialise the hipEvent_t handles (torch creates them lazily)
+            a.record()
+            b.record()
         torch.cuda.synchronize(dev)
 
-    def step(i, timed):
+    def step(i, ev=None):
+        s = sets[i % nsets]
+        if cpu:
+            pass_.full(s)
+            return
         if graphs:
-            graphs[i % len(graphs)].replay()
+            graphs[i % nsets].replay()
         else:
-            one_pass(sets[i % nsets], evs[i] if timed else None)
+            pass_.pre(s)
+        pass_.corr_l4(s, ev)
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize(dev)
 
     for i in range(args.warmup):
-        step(i, False)
+        step(i)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i, True)
-    torch.cuda.synchronize(dev)
+        step(i, None if cpu else evs[i])
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, device=dev)  # MAX over ranks (no-op at N=1)
 
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    # ---- replay self-check: poison one set's outputs, run one step, compare with fresh ----
+    k = (args.steps - 1) % nsets
+    s = sets[k]
+    for lv in s:
+        lv["corr"].fill_(float("nan"))
+    step(k)
+    sync()
+    ref = pass_.fresh(s)
+    replay_diff = [_diff(lv["corr"], r) for lv, r in zip(s, ref)]
+    replay_ok = all(d <= 1e-5 for d in replay_diff)
+    shards = shard_check(pass_, shapes, B, world, rank, dev, dtype)
+    if world > 1:
+        flag = torch.tensor([int(replay_ok)], device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        replay_ok = bool(flag.item())
+
+    C4, h4, w4 = shapes[-1]
     pairs = B * args.steps * world
     value = pairs / elapsed
-    bytes_launch = corr_bytes_per_pair(C4, h4, w4, esz) * B
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(args.pmc) if args.dtype == "fp32" and B == 8 else None
-
     result = {
         "metric": "image-pairs/sec (forward, 384x448): hot path = WarpingLayer + Correlation(d=4)"
                   " at all 5 pyramid levels; lvl2 corr HBM GB/s vs peak",
@@ -264,34 +541,49 @@ def main():
             "per_gpu_batch": B,
             "height": args.height,
             "width": args.width,
-            "levels": [list(s) for s in shapes],
+            "levels": [list(x) for x in shapes],
             "parallelism": f"dp{world} (batch-sharded replicas, no data-path collective)",
             "buffer_sets": nsets,
             "fused_levels": sorted(fused),
             "graph": bool(graphs),
+            "device": "cpu (launcher rehearsal: torch-CPU stand-in, not the product path)"
+                      if cpu else "cuda",
         },
-        "roofline": {
-            "kernel": "corr_fwd_ring<RingN> at l4 (32x96x112, B=8)",
+        "checks": {"replay": replay_ok, "replay_max_rel_diff": replay_diff, "shards": shards,
+                   "weights_broadcast": bcast},
+    }
+    if not cpu:
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        bytes_launch = corr_bytes_per_pair(C4, h4, w4, esz) * B
+        achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+        traffic, tsrc = (load_pmc_traffic(args.pmc) if args.dtype == "fp32" and B == 8
+                         and (args.height, args.width) == (384, 448) else (None, None))
+        result["roofline"] = {
+            "kernel": "l4 correlation (32x96x112, B=8), hipExtLaunchKernel events per timed step",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": tsrc,
             "algorithmic_bytes_per_launch": bytes_launch,
             "avg_launch_us": round(kern_ms * 1e3, 3),
-        },
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(
-            16, len(os.sched_getaffinity(0)))
-        result["cpu_baseline"] = cpu_baseline(shapes, B, args.cpu_seconds, threads)
+        }
+    if rank == 0 and world == 1 and not cpu and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_torch(shapes, B, args.cpu_seconds)
         result["cpu_baseline"]["speedup"] = round(value / result["cpu_baseline"]["value"], 1)
+        thr = torch.get_num_threads()
+        result["cpu_baseline_port"] = cpu_baseline_port(shapes, B, args.cpu_seconds / 2, thr)
+    ok = replay_ok and (shards is None or shards["ok"]) and (bcast is None or bcast["ok"])
     if rank == 0:
         print(json.dumps(result), flush=True)
+        if not ok:
+            print("bench.py: self-check FAILED", file=sys.stderr)
     if world > 1:
         dist.destroy_process_group()
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -6,7 +6,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "../../include/pwc_hotpath.h"
 #include "pwc_common.cuh"
@@ -33,6 +35,26 @@ hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void
 }  // namespace pwc
 
 namespace pwc {
+// PWC_DEBUG="name=value,..." (pwc_common.cuh), parsed once on first use.
+int debug_knob(const char* name, int def) {
+  static const std::string spec = [] {
+    const char* e = std::getenv("PWC_DEBUG");
+    return std::string(e ? e : "");
+  }();
+  if (spec.empty()) return def;
+  const size_t n = std::strlen(name);
+  size_t pos = 0;
+  while (pos < spec.size()) {
+    size_t end = spec.find(',', pos);
+    if (end == std::string::npos) end = spec.size();
+    const std::string item = spec.substr(pos, end - pos);
+    if (item.size() > n + 1 && item.compare(0, n, name) == 0 && item[n] == '=')
+      return std::atoi(item.c_str() + n + 1);
+    pos = end + 1;
+  }
+  return def;
+}
+
 // output epilogue of the next correlation launch of this thread (pwc_corr_forward_into)
 thread_local OutEpi g_epi = {0, 1.f};
 OutEpi current_epi() { return g_epi; }

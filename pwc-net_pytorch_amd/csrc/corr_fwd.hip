@@ -520,6 +520,10 @@ hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void
 hipError_t corr_forward_rows_f32(const void*, const void*, void*, int, int, int, int, float,
                                  hipStream_t);
 
+// corr_stream.hip: full-width row bands + loader wave (the l4-sized grids; it decides).
+hipError_t corr_forward_stream_f32(const void*, const void*, void*, int, int, int, int, int,
+                                   float, hipStream_t);
+
 // corr_rows.hip (row bands over full rows) serves l3-sized grids (it decides; PWC_ROWS).
 
 // PWC_CORR_GRP=0 disables the coarse-level kernel (measurement of the split path only).
@@ -547,6 +551,12 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
   // a strided / activated output (pwc_corr_forward_into) is written by the band, row-band,
   // parity-tile and ring kernels only; every other path declines before launching
   const bool epi_def = epi_is_default(current_epi());
+  if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && s2 == 2 && pad == md &&
+      (md == 8 || md == 9)) {
+    const hipError_t e = corr_forward_stream_f32(in1, in2, out, B, C, H, W, layout, divisor,
+                                                 stream);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && layout == kRaster &&
       s2 == 2 && pad == md && (md == 8 || md == 9) &&
       (band_mode() == 2 || (band_mode() == 1 && (H + 1) / 2 <= 6))) {

@@ -129,6 +129,11 @@ __device__ __forceinline__ float epi_act(float v, float slope) { return v > 0.f 
 OutEpi current_epi();
 inline bool epi_is_default(const OutEpi& e) { return e.ostride == 0 && e.slope == 1.f; }
 
+// Debug / measurement knobs: ONE environment variable, PWC_DEBUG="name=value,name=value",
+// parsed once per process (capi.hip).  Unset knobs return `def`; production runs set nothing.
+// Kernels never read it -- launchers turn a knob into a template choice or an argument.
+int debug_knob(const char* name, int def);
+
 // XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle must
 // be bijective"): consecutive logical tiles land on the same XCD (and L2), so neighbouring
 // tiles that re-read each other's halo rows hit the same L2.  Pure speed choice.

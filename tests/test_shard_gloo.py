@@ -88,3 +88,38 @@ def test_two_rank_sharded_hot_path_matches_single_process():
     assert r0[1] == 0.0 and r0[2] == (5, 81, 12, 14)  # bit-identical: same per-item arithmetic
     assert r0[3] == r1[1]                               # parameters broadcast from rank 0
     assert r0[4] == r1[2] == 2.0                        # max over ranks
+
+
+def test_bench_launcher_two_ranks_cpu_rehearsal():
+    """bench.py --gpus 2 starts its own two ranks (torch.distributed.run child), shards the
+    checked pairs, broadcasts the Net harness weights from rank 0 and verifies every rank's
+    per-pair checksums against rank 0's recomputation (launcher rehearsal on gloo, with the
+    torch-CPU stand-in for the per-shard op)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--device", "cpu",
+                        "--gpus", "2", "--height", "128", "--width", "128", "--batch", "2",
+                        "--steps", "2", "--warmup", "1"], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4
+    assert d["checks"]["replay"] is True
+    assert d["checks"]["shards"] == {"pairs": 4, "ranks": 2, "ok": True, "bad_ranks": []}
+    assert d["checks"]["weights_broadcast"]["ok"] is True
+    assert d["checks"]["weights_broadcast"]["bytes"] == 20475776  # SURVEY §8e
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--device", "cpu",
+                        "--gpus", "2"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr

@@ -19,7 +19,7 @@
 #include <string>
 #include <vector>
 
-#include "../pwc-net_pytorch_amd/csrc/corr_par.hip"
+#include "corr_par.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_ring.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_pt.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_grp.hip"
