@@ -12,9 +12,8 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .ops import (CorrelationCatFunction, CorrelationFunction, CostVolumeFunction,
-                  UpsampleWarpFunction,
-                  WarpCorrelationFunction, WarpFunction)
+from . import library as _library  # registers torch.ops.pwcnet.* (traceable single nodes)
+from .ops import (CorrelationCatFunction, UpsampleWarpFunction, WarpCorrelationFunction)
 
 
 class Correlation(nn.Module):
@@ -36,9 +35,13 @@ class Correlation(nn.Module):
         self.corr_multiply = corr_multiply
 
     def forward(self, input1, input2):
-        return CorrelationFunction.apply(input1, input2, self.pad_size, self.kernel_size,
-                                         self.max_displacement, self.stride1, self.stride2,
-                                         self.corr_multiply)
+        # functions/correlation.py:17-18 asserts contiguity; the op (torch.ops.pwcnet.
+        # correlation, autograd registered) is CorrelationFunction's traceable twin
+        assert input1.is_contiguous()
+        assert input2.is_contiguous()
+        return _library.correlation(input1, input2, self.pad_size, self.kernel_size,
+                                    self.max_displacement, self.stride1, self.stride2,
+                                    self.corr_multiply)
 
     def extra_repr(self):
         return (f"pad_size={self.pad_size}, kernel_size={self.kernel_size}, "
@@ -59,7 +62,7 @@ class WarpingLayer(nn.Module):
         self.args = args
 
     def forward(self, x, flow):
-        return WarpFunction.apply(x, flow)
+        return _library.warp(x, flow)
 
 
 class WarpCorrelation(nn.Module):
@@ -138,7 +141,7 @@ class CostVolumeLayer(nn.Module):
         self.search_range = args.search_range
 
     def forward(self, src, tgt):
-        return CostVolumeFunction.apply(src, tgt, self.search_range)
+        return _library.cost_volume(src, tgt, self.search_range)
 
 
 def get_grid(x: torch.Tensor) -> torch.Tensor:

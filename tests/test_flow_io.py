@@ -58,3 +58,14 @@ def test_vis_flow_known_answers():
     img2 = vis_flow(f2)
     assert f2[0, 2, 0] == 2e9
     assert np.array_equal(img2, img)
+
+
+def test_vis_flow_matches_reference_fixture():
+    """flow_utils.vis_flow run in the build container (cv2 stubbed; gen_golden.py) on a flow
+    with unknown (> 1e9) entries and a zero vector: identical uint8 image."""
+    import os
+    from conftest import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "visflow_20x24.npz"))
+    img = vis_flow(z["flow"])
+    assert img.dtype == np.uint8 and img.shape == z["img"].shape
+    np.testing.assert_array_equal(img, z["img"])

@@ -11,6 +11,12 @@ import numpy as np
 import pytest
 import torch
 
+
+def _seed(*parts):
+    """Process-independent seed (str hashing is randomised per process; crc32 is not)."""
+    import zlib
+    return zlib.crc32(repr(parts).encode())
+
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -64,7 +70,7 @@ def _check(a, b, f, out, x2w, md=9):
 def test_fused_vs_oracle(shape, band_cfg):
     from pwcnet_amd.ops import warp_corr_forward, warp_forward
     B, C, H, W = shape
-    a, b, f = _inputs(hash((shape, band_cfg)) % 2**32, *shape)
+    a, b, f = _inputs(_seed(shape, band_cfg), *shape)
     out, x2w = warp_corr_forward(_t(a), _t(b), _t(f), 9, 1, 9, 1, 2)
     torch.cuda.synchronize()
     _check(a, b, f, out, x2w)
@@ -174,4 +180,4 @@ def test_warp_correlation_module_autograd():
     gx2, gfl = O.warp_backward(b, f, gw + gw_extra)
     np.testing.assert_allclose(_np(x1.grad), g1, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(_np(x2.grad), gx2, rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(_np(fl.grad), gfl, rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(_np(fl.grad), gfl, rtol=1e-4, atol=1e-4)  # config 5
