@@ -358,6 +358,35 @@ def cpu_baseline_torch(shapes, B, seconds):
                        f"l0-l4 of 384x448, fp32, torch.get_num_threads()={thr}")
 
 
+def cpu_config1(seconds):
+    """BASELINE config 1: the reference's whole predict forward on CPU -- model.py's Net with
+    corr = CostVolumeLayer (pure PyTorch correlation + grid_sample), reference defaults, one
+    centre-cropped example pair (example/1.png, 2.png -> 384x448, main.py:321-327; committed
+    as tests/golden/example_crops_384x448.npz), random-init weights (no checkpoint)."""
+    import warnings
+    from oracle import torch_ref as T
+    z = np.load(os.path.join(ROOT, "tests", "golden", "example_crops_384x448.npz"))
+    x = torch.from_numpy(np.stack([z["img1"], z["img2"]])).float()  # 2 x H x W x 3
+    x = x.permute(3, 0, 1, 2).unsqueeze(0).contiguous()            # 1 x 3 x 2 x H x W
+    net = T.reference_cpu_net()
+    times = []
+    with torch.no_grad(), warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        net(x, fused=False)  # warm-up
+        t_end = time.perf_counter() + seconds
+        while True:
+            t0 = time.perf_counter()
+            net(x, fused=False)
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() >= t_end or len(times) >= 20:
+                break
+    med = float(np.median(times))
+    return dict(value=round(1.0 / med, 3), unit="image-pairs/s", ms_per_pair=round(med * 1e3, 1),
+                cores=torch.get_num_threads(), kind="port",
+                sample=f"median of {len(times)} full Net forwards (convs + CostVolumeLayer + "
+                       "grid_sample) on the cropped example pair, B=1, fp32 CPU")
+
+
 def cpu_baseline_port(shapes, B, seconds, threads):
     """fp32 C port of the GPU semantics (warp + Corr9, oracle/pwc_oracle.c, OpenMP)."""
     from oracle import oracle as O
@@ -575,6 +604,7 @@ def main(argv=None):
         result["cpu_baseline"]["speedup"] = round(value / result["cpu_baseline"]["value"], 1)
         thr = torch.get_num_threads()
         result["cpu_baseline_port"] = cpu_baseline_port(shapes, B, args.cpu_seconds / 2, thr)
+        result["cpu_config1"] = cpu_config1(args.cpu_seconds / 2)
     ok = replay_ok and (shards is None or shards["ok"]) and (bcast is None or bcast["ok"])
     if rank == 0:
         print(json.dumps(result), flush=True)

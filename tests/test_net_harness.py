@@ -22,14 +22,11 @@ from pwcnet_amd.net import Net, NetArgs
 FIX = os.path.join(GOLDEN, "net_cvl_128x128.npz")
 
 
-class _RefWarp(nn.Module):
-    def forward(self, x, flow):
-        return T.warp(x, flow)
+_RefWarp = T.RefWarpingLayer
 
 
-class _RefCVL(nn.Module):
-    def forward(self, src, tgt):
-        return T.cost_volume(src, tgt, 4)
+def _RefCVL():
+    return T.RefCostVolumeLayer(4)
 
 
 class _RefCorr9(nn.Module):
