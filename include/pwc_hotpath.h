@@ -57,7 +57,8 @@ extern "C" {
 #define PWC_DTYPE_BF16 2
 
 /* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
- * 4: fused warp -> correlation, 5: fused flow upsample -> warp, corr into a slice). */
+ * 4: fused warp -> correlation, 5: fused flow upsample -> warp, corr into a slice,
+ * 6: pwc_set_debug). */
 PWC_API int pwc_abi_version(void);
 
 /* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
@@ -65,6 +66,13 @@ PWC_API int pwc_abi_version(void);
  * (hipEvent_t, timing enabled) at that kernel's start and end on its stream.  One-shot; pass
  * (NULL, NULL) to disarm.  Used by bench.py to time the dominant kernel live. */
 PWC_API int pwc_time_next_corr(void* start_event, void* stop_event);
+
+/* Measurement / test hook: replace the debug knob string (initially the PWC_DEBUG environment
+ * variable; "name=value,name=value", integer values; NULL or "" = production defaults).  Knobs
+ * only select among equivalent kernel variants (tests run every variant against the oracle)
+ * or disable work for ablation timings; no knob is set in production.  Not thread-safe with
+ * concurrent launches. */
+PWC_API int pwc_set_debug(const char* spec);
 
 /* Last error message of the calling thread ("" if none). */
 PWC_API const char* pwc_last_error(void);
@@ -136,8 +144,12 @@ PWC_API int pwc_cost_volume_backward(const void* src, const void* tgt, const voi
  * flow is [B][2][H][W], channel 0 = u (horizontal), 1 = v (vertical), in pixels. */
 PWC_API int pwc_warp_forward(const void* x, const void* flow, void* out, int B, int C, int H, int W,
                      int dtype, void* stream);
-/* grad_x is zeroed on `stream` and accumulated with fp32 atomics (as ATen's
- * grid_sampler_2d_backward); grad_flow is written element-wise. */
+/* Adjoint of pwc_warp_forward (ATen grid_sampler_2d_backward with the reference's grid chain).
+ * grad_x: every element is written once (no memset, no atomics): per 8x32 tile of grad_x the
+ * output pixels whose bilinear corners land in the tile are gathered in fixed order (a
+ * counting sort in LDS), so the result is deterministic.  grad_flow: per pixel, element-wise;
+ * only corners that fall outside the gather window of their tile (flows beyond ~8 px) are
+ * added with fp32 atomics.  fp32 only. */
 PWC_API int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, void* grad_x,
                       void* grad_flow, int B, int C, int H, int W, int dtype, void* stream);
 

@@ -35,12 +35,19 @@ hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void
 }  // namespace pwc
 
 namespace pwc {
-// PWC_DEBUG="name=value,..." (pwc_common.cuh), parsed once on first use.
-int debug_knob(const char* name, int def) {
-  static const std::string spec = [] {
+// PWC_DEBUG="name=value,..." (pwc_common.cuh): read from the environment once, replaceable by
+// pwc_set_debug() (tests / measurement tools); empty in production, where every knob returns
+// its default without parsing anything.
+std::string& debug_spec() {
+  static std::string spec = [] {
     const char* e = std::getenv("PWC_DEBUG");
     return std::string(e ? e : "");
   }();
+  return spec;
+}
+
+int debug_knob(const char* name, int def) {
+  const std::string& spec = debug_spec();
   if (spec.empty()) return def;
   const size_t n = std::strlen(name);
   size_t pos = 0;
@@ -123,22 +130,19 @@ bool corr_shape(int H, int W, int pad, int k, int md, int s1, int s2, int* oc, i
 // Kernel-selection override for cross-checks (env PWC_CORR_PATH, read once):
 //   "generic" (1): literal one-thread-per-output kernels only;
 //   "regtile" (2): skip the LDS-DMA ring kernel, use the register-staged tiled kernel.
-int force_generic() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = std::getenv("PWC_CORR_PATH");
-    v = 0;
-    if (s && std::strcmp(s, "generic") == 0) v = 1;
-    if (s && std::strcmp(s, "regtile") == 0) v = 2;
-  }
-  return v;
-}
+// knob corr_path: 1 = literal per-element kernel, 2 = register-tiled kernel (measurement)
+int force_generic() { return pwc::debug_knob("corr_path", 0); }
 
 }  // namespace
 
 extern "C" {
 
-int pwc_abi_version(void) { return 5; }
+int pwc_abi_version(void) { return 6; }
+
+int pwc_set_debug(const char* spec) {
+  pwc::debug_spec() = spec ? spec : "";
+  return 1;
+}
 
 int pwc_time_next_corr(void* start_event, void* stop_event) {
   if ((start_event == nullptr) != (stop_event == nullptr))
@@ -516,14 +520,7 @@ static bool warp_corr_fusable(int pad, int k, int md, int s1, int s2, int dtype)
          (md == 8 || md == 9);
 }
 
-static int fused_disabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = std::getenv("PWC_FUSED");
-    v = (s && s[0] == '0') ? 1 : 0;
-  }
-  return v;
-}
+static int fused_disabled() { return pwc::debug_knob("fused", 1) == 0; }
 
 static size_t elem_size(int dtype) { return dtype == PWC_DTYPE_F32 ? 4 : 2; }
 

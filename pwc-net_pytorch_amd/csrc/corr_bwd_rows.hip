@@ -268,10 +268,7 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
                                   void* g2, int B, int C, int H, int W, float divisor,
                                   hipStream_t stream) {
   using namespace bwdrows;
-  static const bool off = [] {
-    const char* e = std::getenv("PWC_BWD_ROWS");
-    return e && e[0] == '0';
-  }();
+  const bool off = debug_knob("bwd_rows", 1) == 0;
   if (off || B == 0 || C == 0 || H == 0 || W < 2) return hipErrorNotSupported;
   if ((size_t)C * H * W >= (1ull << 29) || (size_t)81 * H * W >= (1ull << 29))
     return hipErrorNotSupported;
@@ -293,7 +290,8 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
     R = r;
     break;
   }
-  if (const char* e = std::getenv("PWC_BWD_CFG")) std::sscanf(e, "%d,%d", &R, &CT);
+  R = debug_knob("bwd_r", R);
+  CT = debug_knob("bwd_ct", CT);
   g.R = R;
   g.I = 9 * R * 2 * g.S;
   if (R < 1 || g.I > NT) return hipErrorNotSupported;
@@ -316,7 +314,7 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   const int nchunks = (C + g.ck - 1) / g.ck;
   int nsl = 1;
   while (nsl < nchunks && bands * (nsl + 1) <= 320) ++nsl;  // measured: 1 at l4, 2 at l3
-  if (const char* e = std::getenv("PWC_BWD_SLICES")) nsl = std::max(1, std::min(nchunks, std::atoi(e)));
+  if (const int k = debug_knob("bwd_slices", 0)) nsl = std::max(1, std::min(nchunks, k));
   g.cps = ((nchunks + nsl - 1) / nsl) * g.ck;
   nsl = (C + g.cps - 1) / g.cps;
   g.inv_lw = 1.f / (float)g.lw;

@@ -492,27 +492,13 @@ size_t corr_workspace_bytes(int B, int OC, int Ho, int Wo) {
 }
 
 // PWC_CORR_PT=0 disables the parity-tile kernel (measurement of the older paths).
-static bool pt_disabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = std::getenv("PWC_CORR_PT");
-    v = (s && s[0] == '0') ? 1 : 0;
-  }
-  return v == 1;
-}
+static bool pt_disabled() { return debug_knob("corr_pt", 1) == 0; }
 
 // The band kernel of warp_corr.hip (without the warp) serves model.py:24's correlation at the
 // smallest levels (parity half of <= 6 rows: l0, l1 at 384x448; measured 6.8 / 7.8 us against
 // 11.0 / 13.4 us for corr_small + its reduce).  PWC_CORR_BAND=0 disables it, =1 forces it at
 // every size (measurement).
-static int band_mode() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = std::getenv("PWC_CORR_BAND");
-    v = (s && s[0] == '0') ? 0 : (s && s[0] == '1') ? 2 : 1;
-  }
-  return v;
-}
+static int band_mode() { return debug_knob("corr_band", 1); }
 
 hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                               int, float, int, hipStream_t);
@@ -527,14 +513,7 @@ hipError_t corr_forward_stream_f32(const void*, const void*, void*, int, int, in
 // corr_rows.hip (row bands over full rows) serves l3-sized grids (it decides; PWC_ROWS).
 
 // PWC_CORR_GRP=0 disables the coarse-level kernel (measurement of the split path only).
-static bool grp_disabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = std::getenv("PWC_CORR_GRP");
-    v = (s && s[0] == '0') ? 1 : 0;
-  }
-  return v == 1;
-}
+static bool grp_disabled() { return debug_knob("corr_grp", 1) == 0; }
 
 // `workspace` (>= corr_workspace_bytes) enables channel splitting for grids too small to fill
 // the chip; null keeps one workgroup per tile over all channels.

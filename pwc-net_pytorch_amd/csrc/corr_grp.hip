@@ -355,14 +355,7 @@ using GFd = GrpTile<1, 8, 1, 6, true>;
 using GGd = GrpTile<1, 4, 2, 4, true>;
 using GHd = GrpTile<3, 2, 3, 6, true>;
 
-int grp_cfg() {
-  static int v = -2;
-  if (v == -2) {
-    const char* s = std::getenv("PWC_GRP_CFG");
-    v = (s && s[0] >= 'A' && s[0] <= 'H' && s[1] == 0) ? s[0] - 'A' : -1;
-  }
-  return v;
-}
+int grp_cfg() { return debug_knob("grp_cfg", -1); }  // 0..7 = A..H (measurement)
 
 }  // namespace grp
 

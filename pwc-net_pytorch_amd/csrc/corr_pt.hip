@@ -436,7 +436,7 @@ hipError_t corr_forward_pt_f32(const void* in1, const void* in2, void* out, int 
   if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16)
     return hipErrorNotSupported;
   if ((size_t)C * H * W * 4 >= 0x7ffffff0ull) return hipErrorNotSupported;
-  if (const char* e = std::getenv("PWC_PT_K")) groups = std::atoi(e);
+  if (const int k = debug_knob("pt_k", 0)) groups = k;
   if (groups <= 0) {
     // the largest tile (fewest halo bytes per output) that still gives ~one tile per CU;
     // grids that fill the chip with single-group tiles stay on corr_ring.hip (measured equal
@@ -447,7 +447,7 @@ hipError_t corr_forward_pt_f32(const void* in1, const void* in2, void* out, int 
       const long long tiles = (long long)B * 2 * ((hp + 24 / k - 1) / (24 / k)) * ntx;
       if (tiles >= 192) { groups = k; break; }
     }
-    static const bool l4 = std::getenv("PWC_PT_L4") && std::getenv("PWC_PT_L4")[0] == '1';
+    const bool l4 = debug_knob("pt_l4", 0) == 1;
     if (groups == 1 && !l4) return hipErrorNotSupported;
   }
   switch (groups) {

@@ -1017,13 +1017,9 @@ using RingPL = RingTile<4, 2, 16, 3, 4, 3>;   // 60 KiB, 2 stages (6 channels) i
 using RingPM = RingTile<4, 2, 16, 2, 5, 2>;   // 50 KiB, 3 stages (6 channels) in flight
 
 static int ring_cfg() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = std::getenv("PWC_RING_CFG");
-    v = 13;  // default: N (3 workgroups per tile; measured 18.3 vs 19.9 us for C at l4, B 8)
-    if (s && s[0] >= 'A' && s[0] <= 'R' && s[1] == 0) v = s[0] - 'A';
-  }
-  return v;
+  // knob ring_cfg = 0..17 (A..R); default 13 = N (3 workgroups per tile; measured 18.3 vs
+  // 19.9 us for C at l4, B 8)
+  return debug_knob("ring_cfg", 13);
 }
 
 // Number of channel splits for a grid of `base_blocks` tiles: none once the tiles alone give

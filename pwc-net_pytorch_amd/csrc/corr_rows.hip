@@ -246,10 +246,7 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
 hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, int B, int C,
                                  int H, int W, float divisor, hipStream_t stream) {
   using namespace rows;
-  static const int mode = [] {
-    const char* e = std::getenv("PWC_ROWS");
-    return (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 2 : 1;
-  }();
+  const int mode = debug_knob("rows", 1);  // 0 off, 2 forced at every size (measurement)
   if (mode == 0) return hipErrorNotSupported;
   if (W % 4 != 0 || W < 8 || B == 0) return hipErrorNotSupported;
   if ((size_t)B * C * H * W >= (1ull << 30) || (size_t)B * 81 * H * W >= (1ull << 31))
@@ -258,8 +255,9 @@ hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, in
   // l3 (24) R 2 -> 14.4 us against 16.1, l4 (48) R 3 -> 18.5 against 19.4 (kbench)
   const int hp0 = (H + 1) / 2;
   int R = hp0 <= 24 ? 2 : 3, CK = 16;
-  if (const char* e = std::getenv("PWC_ROWS_CFG")) {
-    std::sscanf(e, "%d,%d", &R, &CK);
+  if (debug_knob("rows_r", 0) > 0) {
+    R = debug_knob("rows_r", R);
+    CK = debug_knob("rows_ck", CK);
   } else if (hp0 <= 12 || (hp0 > 24 && mode != 2)) {
     return hipErrorNotSupported;
   }

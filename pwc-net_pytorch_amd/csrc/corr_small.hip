@@ -371,7 +371,7 @@ hipError_t corr_forward_small_f32(const void* in1, const void* in2, void* out, i
     if (nsplit > max_splits) nsplit = max_splits;
     if (nsplit < 1) nsplit = 1;
   }
-  if (const char* e = std::getenv("PWC_SMALL_SPLITS")) nsplit = std::atoi(e);
+  if (const int k = debug_knob("small_splits", 0)) nsplit = k;
   // a slice's partial block holds 2 * ceil(Ho / 2) rows: stay inside the caller's workspace,
   // sized for max_splits volumes of Ho rows
   if (nsplit > 1) {

@@ -439,17 +439,10 @@ __global__ __launch_bounds__(256) void warp_bwd_flow(const float* __restrict__ x
   gflow[(2 * n + 1) * plane + pix] = (giy * my) / halfy;
 }
 
-// PWC_WARP_CFG=<digit> selects a (channels per group, groups per thread) variant for
-// measurement: 0 = 4 channels per thread, XCD-grouped pixel blocks (default), 1 = 8, 2 = 2,
+// knob warp_cfg selects a (channels per group, groups per thread) variant for measurement:
+// 0 = 4 channels per thread, XCD-grouped pixel blocks (default), 1 = 8, 2 = 2,
 // 3 = 4 without XCD grouping, 4 = 2 grouped, 5 = 8 grouped.
-static int warp_cfg() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = std::getenv("PWC_WARP_CFG");
-    v = (e && e[0] >= '0' && e[0] <= '9' && e[1] == 0) ? e[0] - '0' : 0;
-  }
-  return v;
-}
+static int warp_cfg() { return debug_knob("warp_cfg", 0); }
 
 template <typename T>
 hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int C, int H,
@@ -485,10 +478,10 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
   if (npix == 0) return hipSuccess;
   if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
   const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
-  static const bool scatter = std::getenv("PWC_WARP_BWD") && std::getenv("PWC_WARP_BWD")[0] == '0';
+  const bool scatter = debug_knob("warp_bwd", 1) == 0;  // 0: ATen-shaped atomic scatter
   if (!scatter) {
-    // grad_x tile shape (PWC_WARP_TILES=<variant> for measurement)
-    static const int tv = std::getenv("PWC_WARP_TILES") ? std::atoi(std::getenv("PWC_WARP_TILES")) : 0;
+    // grad_x tile shape (knob warp_tiles for measurement)
+    const int tv = debug_knob("warp_tiles", 0);
     int th = 8, tw = 32;
     if (C > 0) {
       hipError_t e = hipSuccess;
@@ -514,7 +507,7 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
     // channel groups for grids with few pixels (the coarse levels): ~64K threads or 16 groups
     int ng = 1;
     while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
-    if (const char* e = std::getenv("PWC_WARP_BWD_NG")) ng = std::atoi(e);
+    if (const int k = debug_knob("warp_bwd_ng", 0)) ng = k;
     const int cpg = (C + ng - 1) / ng;
     const unsigned blocks = (unsigned)((npix * ng + 255) / 256);
 #define PWC_FLOW(NGV)                                                                          \

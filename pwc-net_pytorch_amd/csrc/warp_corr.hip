@@ -353,16 +353,14 @@ struct Cfg {
   int R, T;
 };
 
-// PWC_BAND_CFG="R,T[,G]" overrides the per-level choice (measurement).
+// knobs band_r, band_t [, band_g] override the per-level choice (measurement, tests).
 static bool env_cfg(int* R, int* T, int* G) {
-  const char* e = std::getenv("PWC_BAND_CFG");
-  if (!e || !*e) return false;
-  int r = 0, tt = 0, gg = 0;
-  const int k = std::sscanf(e, "%d,%d,%d", &r, &tt, &gg);
-  if (k < 2) return false;
+  const int r = debug_knob("band_r", 0), tt = debug_knob("band_t", 0);
+  if (r <= 0 || tt <= 0) return false;
   *R = r;
   *T = tt;
-  if (k == 3) *G = gg;
+  const int gg = debug_knob("band_g", 0);
+  if (gg > 0) *G = gg;
   return true;
 }
 
@@ -415,8 +413,7 @@ static bool make_geo(int B, int C, int H, int W, int R, int T, int Greq, Geo* g,
   g->inv_W = 1.f / (float)W;
   g->inv_I = 1.f / (float)g->I;
   g->inv_S = 1.f / (float)g->S;
-  const char* ab = std::getenv("PWC_BAND_ABL");
-  g->abl = ab ? std::atoi(ab) : 0;
+  g->abl = debug_knob("band_abl", 0);
   *lds = stage > red ? stage : red;
   return *lds <= 160 * 1024;
 }

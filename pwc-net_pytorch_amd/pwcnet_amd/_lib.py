@@ -32,6 +32,7 @@ SYMBOLS = {
     "pwc_abi_version": (_I, []),
     "pwc_last_error": (ctypes.c_char_p, []),
     "pwc_time_next_corr": (_I, [_P, _P]),
+    "pwc_set_debug": (_I, [ctypes.c_char_p]),
     "pwc_corr_output_shape": (_I, [_I] * 7 + [_IP] * 3),
     "pwc_corr_forward": (_I, [_P, _P, _P] + [_I] * 11 + [_P]),
     "pwc_corr_workspace_size": (_Z, [_I] * 9),
@@ -51,7 +52,7 @@ SYMBOLS = {
     "pwc_corr_forward_into": (_I, [_P, _P, _P, ctypes.c_longlong, ctypes.c_float] + [_I] * 11
                               + [_P, _Z, _P]),
 }
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lock = threading.Lock()
 _lib = None
@@ -99,3 +100,8 @@ def corr_output_shape(H, W, pad, k, md, s1, s2):
                                        ctypes.byref(oh), ctypes.byref(ow)),
           "Correlation")
     return oc.value, oh.value, ow.value
+
+
+def set_debug(spec: str = "") -> None:
+    """Measurement / test hook (pwc_set_debug): knobs as "name=value,...", "" = defaults."""
+    check(load().pwc_set_debug(spec.encode()), "pwc_set_debug")

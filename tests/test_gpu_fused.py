@@ -48,13 +48,16 @@ def _inputs(seed, B, C, H, W, flow_sigma=2.0):
 
 @pytest.fixture
 def band_cfg(request):
-    old = os.environ.get("PWC_BAND_CFG")
-    os.environ["PWC_BAND_CFG"] = request.param
+    """Band kernel configuration "R,T[,G]" through the library's debug knobs (pwc_set_debug:
+    band_r, band_t, band_g); "" = the per-level default."""
+    from pwcnet_amd import _lib
+    spec = ""
+    if request.param:
+        parts = request.param.split(",")
+        spec = ",".join(f"band_{k}={v}" for k, v in zip("rtg", parts))
+    _lib.set_debug(spec)
     yield request.param
-    if old is None:
-        os.environ.pop("PWC_BAND_CFG", None)
-    else:
-        os.environ["PWC_BAND_CFG"] = old
+    _lib.set_debug("")
 
 
 def _check(a, b, f, out, x2w, md=9):

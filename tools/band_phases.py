@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase timeline of the fused band kernel (warp_corr.hip) from in-kernel s_memrealtime stamps.
 
-    PWC_BAND_CFG=3,1 python tools/band_phases.py --level 0
+    PWC_DEBUG=band_r=3,band_t=1 python tools/band_phases.py --level 0
 
 Prints, over the workgroups of one launch: entry-time spread, and per phase (clear+f1 issue,
 staging, compute, reduce, epilogue) the median / max duration, in microseconds (100 MHz clock).
@@ -15,7 +15,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "pwc-net_pytorch_amd"))
 sys.path.insert(0, ROOT)
-os.environ["PWC_BAND_ABL"] = str(int(os.environ.get("PWC_BAND_ABL", "0")) | 256)
+os.environ["PWC_DEBUG"] = ",".join(
+    x for x in (os.environ.get("PWC_DEBUG", ""), "band_abl=256") if x)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -60,7 +61,7 @@ def main():
     rel = (t - t0) / 100.0  # us
     ph = np.diff(rel, axis=1)
     names = ["clear+f1issue", "staging", "compute", "reduce", "epilogue"]
-    out = dict(level=args.level, cfg=os.environ.get("PWC_BAND_CFG", ""), wgs=int(len(t)),
+    out = dict(level=args.level, cfg=os.environ.get("PWC_DEBUG", ""), wgs=int(len(t)),
                event_us=round(a.elapsed_time(b) * 1e3, 2),
                entry_spread_us=round(float(rel[:, 0].max()), 2),
                last_end_us=round(float(rel[:, 5].max()), 2))

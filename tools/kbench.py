@@ -4,7 +4,7 @@
     python tools/kbench.py [--batch 8] [--height 384] [--width 448] [--iters 50]
 
 Prints one JSON line per (level, op) with the mean device time and algorithmic GB/s.  The
-kernel path can be forced with PWC_CORR_PATH=generic|regtile (read once per process).
+kernel path can be forced with PWC_DEBUG=corr_path=1|2 (generic | register-tiled).
 """
 import argparse
 import json
@@ -67,7 +67,7 @@ def main():
     esz = 4 if dt == torch.float32 else 2
     dev = torch.device("cuda:0")
     B = args.batch
-    path = os.environ.get("PWC_CORR_PATH", "default")
+    path = os.environ.get("PWC_DEBUG", "default")
     levels = [int(v) for v in args.levels.split(",")]
     for l, (C, h, w) in enumerate(bench.level_shapes(args.height, args.width)):
         if l not in levels:
@@ -100,7 +100,7 @@ def main():
             med, mean = timeit(lambda s: warp_corr_forward(s["x1"], s["x2"], s["fl"], 9, 1, 9,
                                                            1, 2), sets, args.iters)
             print(json.dumps(dict(level=l, op="warp_corr", shape=[B, C, h, w],
-                                  band=os.environ.get("PWC_BAND_CFG", ""), us=round(med, 2),
+                                  band=os.environ.get("PWC_DEBUG", ""), us=round(med, 2),
                                   min_us=round(mean, 2), gbs=round(fb / (med * 1e-6) / 1e9, 1),
                                   tag=args.tag)))
         if "upwarp" in ops and h % 2 == 0 and w % 2 == 0:
