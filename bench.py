@@ -588,7 +588,8 @@ def main(argv=None):
         traffic, tsrc = (load_pmc_traffic(args.pmc) if args.dtype == "fp32" and B == 8
                          and (args.height, args.width) == (384, 448) else (None, None))
         result["roofline"] = {
-            "kernel": "l4 correlation (32x96x112, B=8), hipExtLaunchKernel events per timed step",
+            "kernel": f"l4 correlation ({C4}x{h4}x{w4}, B={B}, {args.dtype}), start/stop events "
+                      "per timed step",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,

@@ -182,6 +182,8 @@ static int corr_forward_impl(const char* fn, const void* in1, const void* in2, v
     return fail(fn, "workspace smaller than pwc_corr_workspace_size()");
   const float divisor = (float)(kernel_size * kernel_size * C);  // cu:65 nelems
   hipStream_t s = (hipStream_t)stream;
+  // pwc_time_next_corr: the main correlation kernel of every path launches with the armed
+  // events (hipExtLaunchKernel: exact kernel start/stop, no extra stream packets)
   hipError_t e;
   switch (dtype) {
     case PWC_DTYPE_F32:
@@ -203,6 +205,7 @@ static int corr_forward_impl(const char* fn, const void* in1, const void* in2, v
     default:
       return fail(fn, "unsupported dtype");
   }
+  pwc::g_ev_start = pwc::g_ev_stop = nullptr;  // one-shot, consumed or not
   return check_launch(fn, e);
 }
 

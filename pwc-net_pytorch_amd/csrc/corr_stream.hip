@@ -57,15 +57,20 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int round64(int v) { return (v + 63) / 64 * 64; }
 
-// R: output rows per workgroup (one row parity); W4: image width in quads (W / 4);
-// CC: channels per ring stage; NS: ring depth in stages.
-template <int R_, int W4_, int CC_, int NS_>
+// S2: displacement stride (2: Correlation(9,1,9,1,2) of model.py:24, rows of ONE parity per
+// workgroup; 1: Correlation(4,1,4,1,1) / CostVolumeLayer(sr=4), consecutive rows);
+// R: output rows per workgroup; TW4: column tile width in quads (the tile's 8-pixel segments
+// are the lanes' pixel groups; wider images take several tiles); CC: channels per ring stage;
+// NS: ring depth in stages.
+template <int S2_, int R_, int TW4_, int CC_, int NS_>
 struct Geo {
-  static constexpr int R = R_, W4 = W4_, CC = CC_, NS = NS_;
-  static constexpr int NSEG = W4 / 2;                  // 8-pixel segments per row
+  static constexpr int S2 = S2_, R = R_, TW4 = TW4_, CC = CC_, NS = NS_;
+  static constexpr int NPY = S2 == 2 ? 2 : 1;          // row parities split over workgroups
+  static constexpr int NSEG = TW4 / 2;                 // 8-pixel segments per tile row
   static constexpr int NB = (NSEG + 7) / 8;            // segment blocks per unit
   static constexpr int BS = (NSEG + NB - 1) / NB;      // segments per block (<= 8)
-  static constexpr int S = W4 + 5;                     // LDS row stride in quads (odd)
+  static constexpr int S = TW4 + 5;                    // LDS row stride in quads (odd): 2 halo
+                                                       // quads each side + 1 pad
   static constexpr int F2R = R + 8;                    // f2 rows (tj = -4..4)
   static constexpr int F2Q = round64(F2R * S);         // quads of the f2 part of a channel
   static constexpr int F1Q = round64(R * S);
@@ -79,14 +84,15 @@ struct Geo {
   static constexpr int THREADS = 64 * (NWC + 1);       // + the loader wave
   static constexpr int SLOT_B = CC * CH_B;             // one ring stage
   static constexpr int RING_B = NS * SLOT_B;
-  static constexpr int OUT_B = 81 * R * W4 * 16;       // output staging (after the loop)
+  static constexpr int OUT_B = 81 * R * TW4 * 16;      // output staging (after the loop)
   static constexpr int LDS_BYTES = RING_B > OUT_B ? RING_B : OUT_B;
   static constexpr int NBASE = (RING_B + 32767) / 32768;  // 32 KiB address windows
-  static_assert(W4 % 2 == 0 && BS <= 8, "8-pixel segments, <= 8 per block");
-  static_assert(S % 2 == 1, "odd row stride");
   // loader: wait until stage k landed = at most the later stages' DMAs outstanding, capped by
   // the 6-bit vmcnt (a smaller count only waits a little longer)
   static constexpr int WAITN = (NS - 3) * CC * IPC < 63 ? (NS - 3) * CC * IPC : 63;
+  static_assert(S2 == 1 || S2 == 2, "displacement stride");
+  static_assert(TW4 % 2 == 0 && BS <= 8, "8-pixel segments, <= 8 per block");
+  static_assert(S % 2 == 1, "odd row stride");
   static_assert(NS >= 4, "ring depth");
   static_assert(THREADS <= 1024 && LDS_BYTES <= 160 * 1024, "workgroup resources");
   static_assert(CH_B <= 32768, "a channel fits one 32 KiB window");
@@ -156,25 +162,31 @@ __device__ __forceinline__ void lgk_wait(f32x4 (&w)[6], f32x4 (&f)[2]) {
                : "n"(N));
 }
 
-// Displacements ti in [T0, T1) of one channel: acc[ti][p] += f1[p] * win[p + 2 ti], p = 0..7,
-// as v_pk_fma_f32 (pixel pairs (p, p+1) with p even meet window pairs (p+2ti, p+2ti+1) --
-// aligned register pairs).
-template <int T0, int T1>
+// Displacements ti in [T0, T1) of one channel: acc[ti][p] += f1[p] * win[p + S2 ti], p = 0..7,
+// win[0] = column x0 - 4 S2.  Stride 2: every pixel pair (p, p+1), p even, meets an aligned
+// window pair -> v_pk_fma_f32.  Stride 1: odd ti meet misaligned pairs -> two v_fma_f32 (the
+// same FMA throughput as one v_pk_fma_f32).
+template <int S2, int T0, int T1>
 __device__ __forceinline__ void fma_ti(float (&acc)[9][8], const f32x4 (&w)[6],
                                        const f32x4 (&f)[2]) {
 #pragma unroll
   for (int ti = T0; ti < T1; ++ti) {
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-      const int p = 2 * h, j = p + 2 * ti;
-      const f32x4 q = w[j >> 2];
-      const f32x2 w2 = (j & 2) ? f32x2{q.z, q.w} : f32x2{q.x, q.y};
+      const int p = 2 * h, j = p + S2 * ti;
       const f32x4 a = f[h >> 1];
       const f32x2 a2 = (h & 1) ? f32x2{a.z, a.w} : f32x2{a.x, a.y};
-      f32x2 c2 = {acc[ti][p], acc[ti][p + 1]};
-      c2 = __builtin_elementwise_fma(a2, w2, c2);
-      acc[ti][p] = c2.x;
-      acc[ti][p + 1] = c2.y;
+      if ((j & 1) == 0) {
+        const f32x4 q = w[j >> 2];
+        const f32x2 w2 = (j & 2) ? f32x2{q.z, q.w} : f32x2{q.x, q.y};
+        f32x2 c2 = {acc[ti][p], acc[ti][p + 1]};
+        c2 = __builtin_elementwise_fma(a2, w2, c2);
+        acc[ti][p] = c2.x;
+        acc[ti][p + 1] = c2.y;
+      } else {
+        acc[ti][p] = fmaf(a2.x, w[j >> 2][j & 3], acc[ti][p]);
+        acc[ti][p + 1] = fmaf(a2.y, w[(j + 1) >> 2][(j + 1) & 3], acc[ti][p + 1]);
+      }
     }
   }
 }
@@ -239,17 +251,28 @@ __device__ __forceinline__ void compute_round(const uint32_t (&wa)[G::NBASE],
     // the next channel's eight reads go out in pairs between the FMA chunks, so the LDS queue
     // never holds a wave's whole batch while its FMAs wait to issue
     const uint32_t w_ = wa[WIN], f_ = fa[WIN];
-    if constexpr (!(M & 1)) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
-    if constexpr (!(M & 2)) fma_ti<0, 2>(acc, wc, fc);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!(M & 1)) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
-    if constexpr (!(M & 2)) fma_ti<2, 4>(acc, wc, fc);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!(M & 1)) read2<IMM + 64, IMM + 80>(w_, w_, wn[4], wn[5]);
-    if constexpr (!(M & 2)) fma_ti<4, 6>(acc, wc, fc);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!(M & 1)) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
-    if constexpr (!(M & 2)) fma_ti<6, 9>(acc, wc, fc);
+    if constexpr (G::S2 == 2) {
+      if constexpr (!(M & 1)) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
+      if constexpr (!(M & 2)) fma_ti<2, 0, 2>(acc, wc, fc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(M & 1)) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
+      if constexpr (!(M & 2)) fma_ti<2, 2, 4>(acc, wc, fc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(M & 1)) read2<IMM + 64, IMM + 80>(w_, w_, wn[4], wn[5]);
+      if constexpr (!(M & 2)) fma_ti<2, 4, 6>(acc, wc, fc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(M & 1)) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
+      if constexpr (!(M & 2)) fma_ti<2, 6, 9>(acc, wc, fc);
+    } else {
+      if constexpr (!(M & 1)) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
+      if constexpr (!(M & 2)) fma_ti<1, 0, 3>(acc, wc, fc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(M & 1)) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
+      if constexpr (!(M & 2)) fma_ti<1, 3, 6>(acc, wc, fc);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(M & 1)) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
+      if constexpr (!(M & 2)) fma_ti<1, 6, 9>(acc, wc, fc);
+    }
     if constexpr ((M & 2) != 0) asm volatile("" ::"v"(wc[0]), "v"(wc[5]), "v"(fc[1]));
     // keep this channel's FMAs between its wait and the next channel's (left alone, the
     // scheduler sinks them past later reads and the live ranges overflow into scratch)
@@ -261,16 +284,21 @@ __device__ __forceinline__ void compute_round(const uint32_t (&wa)[G::NBASE],
 template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
-    int C, int H, int W, int Ho, int Wo, int nband, int layout, float divisor,
+    int C, int H, int W, int Ho, int Wo, int nband, int ntx, int layout, float divisor,
     float inv_divisor, OutEpi epi, int abl) {
   static_assert((G::NS * G::CC) % 2 == 0, "buffer parity repeats every round");
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  // logical block = (n, row parity, band, column tile), tile fastest: the tiles and bands of
+  // one image (parity) are neighbours, and xcd_remap keeps neighbours on one XCD (shared halo)
   const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int band = t % nband;
-  const int py = (t / nband) & 1;
-  const int n = t / (2 * nband);
-  const int Y0 = band * G::R;  // first parity row of the band
-  const int nst = C / G::CC;   // ring stages
+  const int tx = t % ntx;
+  const int band = (t / ntx) % nband;
+  const int py = (t / (ntx * nband)) % G::NPY;
+  const int n = t / (ntx * nband * G::NPY);
+  const int Y0 = band * G::R;       // first (parity) row of the band
+  const int X04 = tx * G::TW4;      // first quad of the column tile
+  const int nst = C / G::CC;        // ring stages
+  const int W4 = W >> 2;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -290,10 +318,13 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
     for (int i = 0; i < G::IPC; ++i) {
       const bool f2 = i < G::IF2;
       const int j = (f2 ? 64 * i : 64 * i - G::F2Q) + lane;
-      const int rho = j / G::S, cq = j % G::S - 2;
-      const int srow = f2 ? 2 * (Y0 - 4 + rho) + py : 2 * (Y0 + rho) + py;
-      const bool ok = rho < (f2 ? G::F2R : G::R) && cq >= 0 && cq < G::W4 && srow >= 0 &&
-                      srow < H;
+      // slot quad q of LDS row rho holds image quad X04 - 2 + q (q < TW4 + 4; the last quad
+      // of a row is padding): halo quads come from the neighbouring tile or read zero
+      const int rho = j / G::S, q = j % G::S, cq = X04 - 2 + q;
+      const int prow = f2 ? Y0 - 4 + rho : Y0 + rho;  // parity row (S2 = 2) or row
+      const int srow = G::S2 == 2 ? 2 * prow + py : prow;
+      const bool ok = rho < (f2 ? G::F2R : G::R) && q < G::TW4 + 4 && cq >= 0 && cq < W4 &&
+                      prow >= 0 && srow < H;
       rel[i] = ok ? (uint32_t)(srow * W + 4 * cq) * 4u : kOOB;
     }
     if (abl & 2) {  // measurement: no DMA (barriers only)
@@ -333,9 +364,11 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
     const int seg = blk * G::BS + (sp < G::BS ? sp : 0);
     const bool active = gi < G::NG && sp < G::BS && seg < G::NSEG && (p < 8 || hasb);
     uint32_t wa[G::NBASE], fa[G::NBASE];
+    // window from column x0 - 4 S2: padded quad 2 seg (stride 2) or 2 seg + 1 (stride 1)
+    const int wq = 2 * seg + (G::S2 == 2 ? 0 : 1);
 #pragma unroll
     for (int k = 0; k < G::NBASE; ++k) {
-      wa[k] = lds0 + (uint32_t)(k * 32768 + ((r + tj) * G::S + 2 * seg) * 16);
+      wa[k] = lds0 + (uint32_t)(k * 32768 + ((r + tj) * G::S + wq) * 16);
       fa[k] = lds0 + (uint32_t)(k * 32768 + (G::F2Q + r * G::S + 2 * seg + 2) * 16);
     }
 
@@ -394,14 +427,21 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
 #pragma unroll
           for (int k = 0; k < 8; ++k) acc[ti][k] *= inv_divisor;
       } else {
+        // q = x * (1/d) plus one FMA residual correction: the correctly rounded quotient up to
+        // rare last-ulp ties, at 3 VALU instead of the ~10 of an IEEE division (CostVolumeLayer
+        // divides by 81, modules.py:74)
+        const float rinv = 1.f / divisor;
 #pragma unroll
         for (int ti = 0; ti < 9; ++ti)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) acc[ti][k] /= divisor;
+          for (int k = 0; k < 8; ++k) {
+            const float q = acc[ti][k] * rinv;
+            acc[ti][k] = fmaf(fmaf(-q, divisor, acc[ti][k]), rinv, q);
+          }
       }
 #pragma unroll
       for (int ti = 0; ti < 9; ++ti) {
-        const int oc = out_channel(layout, tj - 4, ti - 4, 4, 9, 2);
+        const int oc = out_channel(layout, tj - 4, ti - 4, 4, 9, G::S2);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           f32x4 v;
@@ -410,7 +450,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
           // odd segment blocks swap their two quads: the two blocks sharing a ds_write_b128
           // lane group (8 consecutive lanes) then hit disjoint 16-B slots
           const int pq = 2 * seg + (h ^ (blk & 1));
-          *reinterpret_cast<f32x4*>(lds + ((oc * G::R + r) * G::W4 + pq) * 4) = v;
+          *reinterpret_cast<f32x4*>(lds + ((oc * G::R + r) * G::TW4 + pq) * 4) = v;
         }
       }
     }
@@ -421,24 +461,24 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
   if (wave == 0) CENSUS(3);  // parked
   if (abl & 4) return;  // measurement: no stores
   float* oimg = out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * Ho * Wo);
-  constexpr int NQ = 81 * G::R * G::W4;
+  constexpr int NQ = 81 * G::R * G::TW4;
   constexpr int PER = (NQ + G::THREADS - 1) / G::THREADS;
   st_f32x4 v[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {  // all LDS reads first, then all stores
     const int q = threadIdx.x + i * G::THREADS;
-    const int xq = q % G::W4, seg = xq >> 1;
+    const int xq = q % G::TW4, seg = xq >> 1;
     const int pq = q - xq + 2 * seg + ((xq & 1) ^ ((seg / G::BS) & 1));  // park swizzle
     if (q < NQ) v[i] = *reinterpret_cast<const st_f32x4*>(lds + 4 * pq);
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int q = threadIdx.x + i * G::THREADS;
-    const int oc = q / (G::R * G::W4);
-    const int rem = q - oc * (G::R * G::W4);
-    const int r = rem / G::W4, xq = rem - r * G::W4;
-    const int y = 2 * (Y0 + r) + py;
-    if (q < NQ && y < Ho) st_out4(oimg + ((size_t)oc * Ho + y) * Wo + 4 * xq, v[i]);
+    const int oc = q / (G::R * G::TW4);
+    const int rem = q - oc * (G::R * G::TW4);
+    const int r = rem / G::TW4, xq = X04 + rem - r * G::TW4;
+    const int y = G::S2 == 2 ? 2 * (Y0 + r) + py : Y0 + r;
+    if (q < NQ && y < Ho && xq < W4) st_out4(oimg + ((size_t)oc * Ho + y) * Wo + 4 * xq, v[i]);
   }
   if (wave == 0) CENSUS(4);  // stores issued
 }
@@ -446,9 +486,10 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
 template <class G>
 static hipError_t launch(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
                          int layout, float divisor, hipStream_t stream) {
-  const int HP = (H + 1) / 2;                  // parity rows (row parity 0 has the extra row)
+  const int HP = G::S2 == 2 ? (H + 1) / 2 : H;  // (parity) rows; parity 0 has the extra row
   const int nband = (HP + G::R - 1) / G::R;
-  const long long nblk = (long long)B * 2 * nband;
+  const int ntx = (W / 4 + G::TW4 - 1) / G::TW4;
+  const long long nblk = (long long)B * G::NPY * nband * ntx;
   if (nblk <= 0) return hipSuccess;
   if (C <= 0 || C % (G::NS * G::CC)) return hipErrorNotSupported;  // whole unrolled rounds
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
@@ -467,33 +508,47 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
   hipExtLaunchKernelGGL((corr_fwd_stream<G>), dim3((unsigned)nblk), dim3(G::THREADS),
                         G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,
-                        (float*)out, C, H, W, H, W, nband, layout, divisor, inv, current_epi(),
-                        debug_knob("stream_abl", 0));
+                        (float*)out, C, H, W, H, W, nband, ntx, layout, divisor, inv,
+                        current_epi(), debug_knob("stream_abl", 0));
   return hipGetLastError();
+}
+
+template <int S2, int TW4>
+static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
+                       int layout, float divisor, hipStream_t stream) {
+  switch (debug_knob("stream_cfg", 0)) {  // measurement variants (R, CC, NS)
+    case 1: return launch<Geo<S2, 3, TW4, 1, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+    case 2: return launch<Geo<S2, 3, TW4, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+    default: return launch<Geo<S2, 3, TW4, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+  }
 }
 
 }  // namespace stream
 
 // hipErrorNotSupported: a shape this kernel does not serve (the caller tries the next path).
-// Serves k = 1, s1 = 1, pad = md (output = input size), dr = 4, s2 = 2, fp32, raster or CVL
-// channel order, 16-B aligned pointers, widths with an instantiated geometry, and grids with
+// Serves k = 1, s1 = 1, pad = md (output = input size) with dr = 4: s2 = 2 (model.py:24's
+// Correlation(9,1,9,1,2)) or s2 = 1 (Correlation(4,1,4,1,1), CostVolumeLayer(sr=4) with the
+// CVL channel order); fp32; W % 4 == 0 and 16-B aligned pointers; C a multiple of 16; grids of
 // at least ~one workgroup per CU (smaller grids have faster homes: corr_pt / corr_rows).
 hipError_t corr_forward_stream_f32(const void* in1, const void* in2, void* out, int B, int C,
-                                   int H, int W, int layout, float divisor, hipStream_t stream) {
-  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16)
+                                   int H, int W, int s2, int layout, float divisor,
+                                   hipStream_t stream) {
+  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16 || W % 4)
     return hipErrorNotSupported;
-  if ((size_t)C * H * W * 4 >= 0x7ffffff0ull) return hipErrorNotSupported;
-  const long long rowsets = (long long)B * 2 * (((H + 1) / 2 + 2) / 3);
-  if (rowsets < 192) return hipErrorNotSupported;
+  if ((size_t)C * H * W * 4 >= 0x7ffffff0ull || C % 16) return hipErrorNotSupported;
+  const int W4 = W / 4;
+  const int tw4 = (W4 % 28 == 0 || W4 < 28) ? 28 : 32;  // 112- or 128-pixel column tiles
+  const long long nblk = (long long)B * (s2 == 2 ? 2 : 1) *
+                         (((s2 == 2 ? (H + 1) / 2 : H) + 2) / 3) * ((W4 + tw4 - 1) / tw4);
+  if (nblk < 192 || W4 < 16) return hipErrorNotSupported;
   using namespace stream;
-  if (W != 112) return hipErrorNotSupported;
-  switch (debug_knob("stream_cfg", 0)) {  // measurement variants (R, CC, NS)
-    case 1: return launch<Geo<3, 28, 1, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    case 2: return launch<Geo<3, 28, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    case 3: return launch<Geo<3, 28, 4, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    case 4: return launch<Geo<2, 28, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    default: return launch<Geo<3, 28, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-  }
+  if (s2 == 2)
+    return tw4 == 28 ? pick<2, 28>(in1, in2, out, B, C, H, W, layout, divisor, stream)
+                     : pick<2, 32>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+  if (s2 == 1)
+    return tw4 == 28 ? pick<1, 28>(in1, in2, out, B, C, H, W, layout, divisor, stream)
+                     : pick<1, 32>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+  return hipErrorNotSupported;
 }
 
 }  // namespace pwc

@@ -1,0 +1,93 @@
+"""BASELINE config 4 (Sintel shape 448x1024, fp16 storage) and the stride-1 correlations at
+full size, through the C ABI, against the fp64 oracle.
+
+fp16: the reference has no fp16 path (correlation_cuda_kernel.cu:5 is fp32 only); the oracle
+runs on the fp16-rounded inputs and the tolerance is the fp16 output rounding (2e-3 relative
+to the volume's max) -- SURVEY §8d config 4.  Shapes at 448x1024 (SURVEY §8 notation):
+l0 192x7x16, l1 128x14x32, l2 96x28x64, l3 64x56x128, l4 32x112x256, plus the north star's
+192x224x32 stress shape (C=32, 192x224, not a pyramid level)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SINTEL = [(2, 192, 7, 16), (2, 128, 14, 32), (2, 96, 28, 64), (2, 64, 56, 128),
+          (2, 32, 112, 256)]
+
+
+def _h(rng, *shape, scale=1.0):
+    return torch.from_numpy((rng.standard_normal(shape) * scale).astype(np.float32)).to(
+        DEV, torch.float16)
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def _close_rel(out, ref, rtol):
+    err = np.abs(out - ref).max() / (np.abs(ref).max() + 1e-12)
+    assert err <= rtol, f"max error {err:.2e} (relative to the max) > {rtol}"
+
+
+@pytest.mark.parametrize("shape", SINTEL, ids=lambda s: "B{}C{}_{}x{}".format(*s))
+def test_sintel_levels_fp16_corr9(shape):
+    from pwcnet_amd.ops import corr_forward
+    rng = np.random.default_rng(40 + shape[2])
+    a, b = _h(rng, *shape), _h(rng, *shape)
+    out = corr_forward(a, b, 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    assert out.dtype == torch.float16 and tuple(out.shape) == (shape[0], 81) + shape[2:]
+    _close_rel(_np(out), O.corr_forward(_np(a), _np(b), 9, 1, 9, 1, 2), 2e-3)
+
+
+@pytest.mark.parametrize("shape", SINTEL[2:], ids=lambda s: "B{}C{}_{}x{}".format(*s))
+def test_sintel_levels_fp16_warp(shape):
+    from pwcnet_amd.ops import warp_forward
+    rng = np.random.default_rng(50 + shape[2])
+    x = _h(rng, *shape)
+    f = _h(rng, shape[0], 2, shape[2], shape[3], scale=3.0)
+    out = warp_forward(x, f)
+    torch.cuda.synchronize()
+    _close_rel(_np(out), O.warp_forward(_np(x), _np(f)), 2e-3)
+
+
+def test_stress_192x224x32_fp16():
+    """The north star's 192x224x32 correlation stress shape (labelled separately from the true
+    level 2 = 112x256x32)."""
+    from pwcnet_amd.ops import corr_forward
+    rng = np.random.default_rng(77)
+    a, b = _h(rng, 2, 32, 192, 224), _h(rng, 2, 32, 192, 224)
+    out = corr_forward(a, b, 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    _close_rel(_np(out), O.corr_forward(_np(a), _np(b), 9, 1, 9, 1, 2), 2e-3)
+
+
+def test_stress_192x224x32_fp32():
+    from pwcnet_amd.ops import corr_forward
+    rng = np.random.default_rng(78)
+    a = rng.standard_normal((2, 32, 192, 224)).astype(np.float32)
+    b = rng.standard_normal((2, 32, 192, 224)).astype(np.float32)
+    out = corr_forward(torch.from_numpy(a).to(DEV), torch.from_numpy(b).to(DEV), 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(out), O.corr_forward(a, b, 9, 1, 9, 1, 2), rtol=1e-5,
+                               atol=1e-5)
+
+
+@pytest.mark.parametrize("sr_cfg", ["corr4", "cvl"])
+def test_stride1_full_size_l4_b8(sr_cfg):
+    """Corr4 = Correlation(4, 1, 4, 1, 1) (the north star's literal d = 4) and CostVolumeLayer
+    (sr = 4, modules.py:53-74) at config 2's l4 size (B=8, 32x96x112), fp32, full compare."""
+    from pwcnet_amd.ops import corr_forward, cost_volume_forward
+    rng = np.random.default_rng(88)
+    a = rng.standard_normal((8, 32, 96, 112)).astype(np.float32)
+    b = rng.standard_normal((8, 32, 96, 112)).astype(np.float32)
+    ta, tb = torch.from_numpy(a).to(DEV), torch.from_numpy(b).to(DEV)
+    if sr_cfg == "corr4":
+        out, ref = corr_forward(ta, tb, 4, 1, 4, 1, 1), O.corr_forward(a, b, 4, 1, 4, 1, 1)
+    else:
+        out, ref = cost_volume_forward(ta, tb, 4), O.cvl_forward(a, b, 4)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(out), ref, rtol=1e-5, atol=1e-5)

@@ -87,6 +87,21 @@ def main():
             print(json.dumps(dict(level=l, op="corr_fwd", path=path, shape=[B, C, h, w],
                                   us=round(med, 2), min_us=round(mean, 2),
                                   gbs=round(cb / (med * 1e-6) / 1e9, 1), tag=args.tag)))
+        # stride-1 correlations (Corr4 = Correlation(4,1,4,1,1), CostVolumeLayer sr=4):
+        # same algorithmic bytes as Corr9 (81 output channels)
+        if "corr4" in ops:
+            med, mean = timeit(lambda s: corr_forward(s["x1"], s["x2"], 4, 1, 4, 1, 1), sets,
+                               args.iters)
+            print(json.dumps(dict(level=l, op="corr4_fwd", shape=[B, C, h, w],
+                                  us=round(med, 2), min_us=round(mean, 2),
+                                  gbs=round(cb / (med * 1e-6) / 1e9, 1), tag=args.tag)))
+        if "cvl" in ops:
+            from pwcnet_amd.ops import cost_volume_forward
+            med, mean = timeit(lambda s: cost_volume_forward(s["x1"], s["x2"], 4), sets,
+                               args.iters)
+            print(json.dumps(dict(level=l, op="cvl_fwd", shape=[B, C, h, w],
+                                  us=round(med, 2), min_us=round(mean, 2),
+                                  gbs=round(cb / (med * 1e-6) / 1e9, 1), tag=args.tag)))
         wb = (2 * C * h * w + 2 * h * w) * B * esz
         if "warp" in ops:
             med, mean = timeit(lambda s: warp_forward(s["x2"], s["fl"]), sets, args.iters)
