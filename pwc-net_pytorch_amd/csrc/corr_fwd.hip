@@ -21,6 +21,7 @@
 #include <hip/hip_ext.h>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "pwc_common.cuh"
 
@@ -515,8 +516,8 @@ hipError_t corr_forward_rows_f32(const void*, const void*, void*, int, int, int,
                                  hipStream_t);
 
 // corr_stream.hip: full-width row bands + loader wave (the l4-sized grids; it decides).
-hipError_t corr_forward_stream_f32(const void*, const void*, void*, int, int, int, int, int,
-                                   int, float, hipStream_t);
+hipError_t corr_forward_stream(const void*, const void*, void*, int, int, int, int, int, int,
+                               int, float, hipStream_t);
 
 // corr_rows.hip (row bands over full rows) serves l3-sized grids (it decides; PWC_ROWS).
 
@@ -538,10 +539,11 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
   // a strided / activated output (pwc_corr_forward_into) is written by the band, row-band,
   // parity-tile and ring kernels only; every other path declines before launching
   const bool epi_def = epi_is_default(current_epi());
-  if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && pad == md && dr == 4 &&
-      (s2 == 1 || s2 == 2)) {
-    const hipError_t e = corr_forward_stream_f32(in1, in2, out, B, C, H, W, s2, layout,
-                                                 divisor, stream);
+  constexpr bool kHalf = std::is_same<T, __half>::value;
+  if (force_generic == 0 && k == 1 && s1 == 1 && (sizeof(T) == 4 || kHalf) && pad == md &&
+      dr == 4 && (s2 == 1 || s2 == 2)) {
+    const hipError_t e = corr_forward_stream(in1, in2, out, B, C, H, W, s2, kHalf ? 1 : 0,
+                                             layout, divisor, stream);
     if (e != hipErrorNotSupported) return e;
   }
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && layout == kRaster &&

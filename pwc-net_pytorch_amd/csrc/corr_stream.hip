@@ -1,6 +1,7 @@
-// corr_stream.hip — correlation forward for model.py:24's Correlation(9, 1, 9, 1, 2) on the
-// finest correlated level (l4 / the paper's "level 2"): full-width row bands, one loader wave
-// streaming channels through an LDS ring, seven compute waves.
+// corr_stream.hip — correlation forward for the large pyramid levels (l4 / the paper's "level
+// 2" and up): row bands over column tiles, one loader wave streaming channels through an LDS
+// ring, seven compute waves; fp32 or fp16 storage, stride-2 (model.py:24's Correlation(9, 1,
+// 9, 1, 2)) or stride-1 (Correlation(4, 1, 4, 1, 1), CostVolumeLayer sr = 4) displacements.
 //
 // Semantics (correlation_cuda_kernel.cu:34-106 with k = 1, s1 = 1, pad = md, dr = 4, s2 = 2):
 //   out[n, (tj+4)*9 + (ti+4), y, x] = sum_c f1[n,c,y,x] * f2[n,c,y+2tj,x+2ti] / C
@@ -54,45 +55,58 @@ __device__ unsigned long long* g_census;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int round64(int v) { return (v + 63) / 64 * 64; }
+constexpr int next_8mod16(int v) { return v + ((8 - v % 16) + 16) % 16; }
 
-// S2: displacement stride (2: Correlation(9,1,9,1,2) of model.py:24, rows of ONE parity per
-// workgroup; 1: Correlation(4,1,4,1,1) / CostVolumeLayer(sr=4), consecutive rows);
-// R: output rows per workgroup; TW4: column tile width in quads (the tile's 8-pixel segments
-// are the lanes' pixel groups; wider images take several tiles); CC: channels per ring stage;
-// NS: ring depth in stages.
-template <int S2_, int R_, int TW4_, int CC_, int NS_>
+// T: storage type (float or __half; arithmetic fp32); S2: displacement stride (2: rows of ONE
+// parity per workgroup; 1: consecutive rows); R: output rows per workgroup; TWP: column tile
+// width in pixels (a lane owns an 8-pixel segment of it; wider images take several tiles);
+// CC: channels per ring stage; NS: ring depth in stages.
+template <typename T, int S2_, int R_, int TWP_, int CC_, int NS_>
 struct Geo {
-  static constexpr int S2 = S2_, R = R_, TW4 = TW4_, CC = CC_, NS = NS_;
-  static constexpr int NPY = S2 == 2 ? 2 : 1;          // row parities split over workgroups
-  static constexpr int NSEG = TW4 / 2;                 // 8-pixel segments per tile row
-  static constexpr int NB = (NSEG + 7) / 8;            // segment blocks per unit
-  static constexpr int BS = (NSEG + NB - 1) / NB;      // segments per block (<= 8)
-  static constexpr int S = TW4 + 5;                    // LDS row stride in quads (odd): 2 halo
-                                                       // quads each side + 1 pad
-  static constexpr int F2R = R + 8;                    // f2 rows (tj = -4..4)
-  static constexpr int F2Q = round64(F2R * S);         // quads of the f2 part of a channel
+  using Elem = T;
+  static constexpr int S2 = S2_, R = R_, TWP = TWP_, CC = CC_, NS = NS_;
+  static constexpr bool H16 = sizeof(T) == 2;
+  static constexpr int EPQ = 16 / (int)sizeof(T);        // elements per 16-B quad
+  static constexpr int NPY = S2 == 2 ? 2 : 1;            // row parities split over workgroups
+  static constexpr int TWQ = TWP / EPQ;                  // tile quads per row
+  static constexpr int HQ = 8 / EPQ;                     // halo quads each side (8 pixels)
+  static constexpr int SQ = 8 / EPQ;                     // quads per 8-pixel segment
+  static constexpr int NSEG = TWP / 8;
+  static constexpr int NB = (NSEG + 7) / 8;              // segment blocks per unit
+  // fp32: balanced blocks; fp16: whole 8-segment blocks (the park swizzle XORs 4 inside one)
+  static constexpr int BS = H16 ? 8 : (NSEG + NB - 1) / NB;
+  // LDS row stride in quads: a ds_read_b128 lane group holds 8 segments of unit A and 8 of a
+  // unit whose row differs by one, so their 16-B slots (mod 256 B) are disjoint iff S is odd
+  // (fp32: 2 quads per segment) or S = 8 mod 16 (fp16: 1 quad per segment)
+  static constexpr int S = H16 ? next_8mod16(TWQ + 2 * HQ) : ((TWQ + 2 * HQ) | 1);
+  static constexpr int NWQ = H16 ? 3 : (S2 == 2 ? 6 : 4);  // window quads read per channel
+  static constexpr int NFQ = H16 ? 1 : 2;                // f1 quads read per channel
+  static constexpr int F2R = R + 8;                      // f2 rows (tj = -4..4)
+  static constexpr int F2Q = round64(F2R * S);           // quads of the f2 part of a channel
   static constexpr int F1Q = round64(R * S);
-  static constexpr int CHQ = F2Q + F1Q;                // quads per channel
+  static constexpr int CHQ = F2Q + F1Q;                  // quads per channel
   static constexpr int CH_B = CHQ * 16;
-  static constexpr int IPC = CHQ / 64;                 // DMA instructions per channel
-  static constexpr int IF2 = F2Q / 64;                 // ... of which read f2
-  static constexpr int NPAIR = 4 * R + (R + 1) / 2;    // unit pairs (see pair_units)
-  static constexpr int NG = NPAIR * NB;                // 16-lane groups
-  static constexpr int NWC = (NG + 3) / 4;             // compute waves
-  static constexpr int THREADS = 64 * (NWC + 1);       // + the loader wave
-  static constexpr int SLOT_B = CC * CH_B;             // one ring stage
+  static constexpr int IPC = CHQ / 64;                   // DMA instructions per channel
+  static constexpr int IF2 = F2Q / 64;                   // ... of which read f2
+  static constexpr int NPAIR = 4 * R + (R + 1) / 2;      // unit pairs (see pair_units)
+  static constexpr int NG = NPAIR * NB;                  // 16-lane groups
+  static constexpr int NWC = (NG + 3) / 4;               // compute waves
+  static constexpr int THREADS = 64 * (NWC + 1);         // + the loader wave
+  static constexpr int SLOT_B = CC * CH_B;               // one ring stage
   static constexpr int RING_B = NS * SLOT_B;
-  static constexpr int OUT_B = 81 * R * TW4 * 16;      // output staging (after the loop)
+  static constexpr int PRQ = H16 ? 8 * NB : TWQ;         // park row quads (output staging)
+  static constexpr int OUT_B = 81 * R * PRQ * 16;
   static constexpr int LDS_BYTES = RING_B > OUT_B ? RING_B : OUT_B;
   static constexpr int NBASE = (RING_B + 32767) / 32768;  // 32 KiB address windows
   // loader: wait until stage k landed = at most the later stages' DMAs outstanding, capped by
   // the 6-bit vmcnt (a smaller count only waits a little longer)
   static constexpr int WAITN = (NS - 3) * CC * IPC < 63 ? (NS - 3) * CC * IPC : 63;
   static_assert(S2 == 1 || S2 == 2, "displacement stride");
-  static_assert(TW4 % 2 == 0 && BS <= 8, "8-pixel segments, <= 8 per block");
-  static_assert(S % 2 == 1, "odd row stride");
+  static_assert(TWP % 8 == 0 && TWP % EPQ == 0 && BS <= 8, "8-pixel segments, <= 8 per block");
+  static_assert(H16 ? S % 16 == 8 : S % 2 == 1, "conflict-free row stride");
   static_assert(NS >= 4, "ring depth");
   static_assert(THREADS <= 1024 && LDS_BYTES <= 160 * 1024, "workgroup resources");
   static_assert(CH_B <= 32768, "a channel fits one 32 KiB window");
@@ -162,10 +176,10 @@ __device__ __forceinline__ void lgk_wait(f32x4 (&w)[6], f32x4 (&f)[2]) {
                : "n"(N));
 }
 
-// Displacements ti in [T0, T1) of one channel: acc[ti][p] += f1[p] * win[p + S2 ti], p = 0..7,
-// win[0] = column x0 - 4 S2.  Stride 2: every pixel pair (p, p+1), p even, meets an aligned
-// window pair -> v_pk_fma_f32.  Stride 1: odd ti meet misaligned pairs -> two v_fma_f32 (the
-// same FMA throughput as one v_pk_fma_f32).
+// fp32, displacements ti in [T0, T1) of one channel: acc[ti][p] += f1[p] * win[p + S2 ti],
+// p = 0..7, win[0] = column x0 - 4 S2.  Stride 2: every pixel pair (p, p+1), p even, meets an
+// aligned window pair -> v_pk_fma_f32.  Stride 1: odd ti meet misaligned pairs -> two
+// v_fma_f32 (the same FMA throughput as one v_pk_fma_f32).
 template <int S2, int T0, int T1>
 __device__ __forceinline__ void fma_ti(float (&acc)[9][8], const f32x4 (&w)[6],
                                        const f32x4 (&f)[2]) {
@@ -191,9 +205,29 @@ __device__ __forceinline__ void fma_ti(float (&acc)[9][8], const f32x4 (&w)[6],
   }
 }
 
+// fp16 storage: the same products from half operands with fp32 accumulation (fma of two
+// widened halves -> v_fma_mix_f32); window element 0 sits at element WEL of quad 0.
+template <int S2, int WEL, int T0, int T1>
+__device__ __forceinline__ void fma_ti_h(float (&acc)[9][8], const f32x4 (&w)[6],
+                                         const f32x4 (&f)[2]) {
+  const f16x8 a = __builtin_bit_cast(f16x8, f[0]);
+  const f16x8 w0 = __builtin_bit_cast(f16x8, w[0]);
+  const f16x8 w1 = __builtin_bit_cast(f16x8, w[1]);
+  const f16x8 w2 = __builtin_bit_cast(f16x8, w[2]);
+#pragma unroll
+  for (int ti = T0; ti < T1; ++ti) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int j = WEL + p + S2 * ti;  // 0..23
+      const _Float16 wv = j < 8 ? w0[j] : j < 16 ? w1[j - 8] : w2[j - 16];
+      acc[ti][p] = fmaf((float)a[p], (float)wv, acc[ti][p]);
+    }
+  }
+}
+
 // One DMA instruction of channel c's slot: `rel` = this lane's byte offset inside the channel
 // plane (or kOOB: the buffer unit returns zeros), `img` = the image's f1 or f2 base.
-__device__ __forceinline__ void dma1(const float* img, uint32_t cbytes, uint32_t img_bytes,
+__device__ __forceinline__ void dma1(const void* img, uint32_t cbytes, uint32_t img_bytes,
                                      uint32_t rel, uint32_t lds_dst) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const int nrec = cbytes < img_bytes ? (int)(img_bytes - cbytes) : 0;
@@ -210,7 +244,7 @@ __device__ __forceinline__ void dma1(const float* img, uint32_t cbytes, uint32_t
 
 template <class G>
 __device__ __forceinline__ void load_stage(int st, uint32_t plane_b, uint32_t img_bytes,
-                                           const float* img1, const float* img2,
+                                           const void* img1, const void* img2,
                                            const uint32_t (&rel)[G::IPC], uint32_t lds0) {
   const uint32_t slot = lds0 + (uint32_t)((st % G::NS) * G::SLOT_B);
 #pragma unroll
@@ -223,12 +257,53 @@ __device__ __forceinline__ void load_stage(int st, uint32_t plane_b, uint32_t im
   }
 }
 
+// One channel's reads (window quads then f1 quads, in pairs) interleaved with its FMA chunks:
+// the next channel's reads go out between the current channel's FMA chunks, so the LDS queue
+// never holds a wave's whole batch while its FMAs wait to issue.  M: measurement modes
+// (launcher knob stream_abl >> 3): 1 no LDS reads, 2 no FMAs, 4 no barriers (only valid
+// without DMA).
+template <class G, int IMM, int M>
+__device__ __forceinline__ void channel_body(uint32_t w_, uint32_t f_, float (&acc)[9][8],
+                                             const f32x4 (&wc)[6], const f32x4 (&fc)[2],
+                                             f32x4 (&wn)[6], f32x4 (&fn)[2]) {
+  constexpr bool RD = !(M & 1), FM = !(M & 2);
+  if constexpr (G::H16) {
+    constexpr int WEL = G::S2 == 2 ? 0 : 4;
+    if constexpr (RD) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
+    if constexpr (FM) fma_ti_h<G::S2, WEL, 0, 5>(acc, wc, fc);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RD) read2<IMM + 32, IMM>(w_, f_, wn[2], fn[0]);
+    if constexpr (FM) fma_ti_h<G::S2, WEL, 5, 9>(acc, wc, fc);
+  } else if constexpr (G::S2 == 2) {
+    if constexpr (RD) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
+    if constexpr (FM) fma_ti<2, 0, 2>(acc, wc, fc);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RD) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
+    if constexpr (FM) fma_ti<2, 2, 4>(acc, wc, fc);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RD) read2<IMM + 64, IMM + 80>(w_, w_, wn[4], wn[5]);
+    if constexpr (FM) fma_ti<2, 4, 6>(acc, wc, fc);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RD) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
+    if constexpr (FM) fma_ti<2, 6, 9>(acc, wc, fc);
+  } else {
+    if constexpr (RD) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
+    if constexpr (FM) fma_ti<1, 0, 3>(acc, wc, fc);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RD) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
+    if constexpr (FM) fma_ti<1, 3, 6>(acc, wc, fc);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RD) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
+    if constexpr (FM) fma_ti<1, 6, 9>(acc, wc, fc);
+  }
+  if constexpr (!FM) asm volatile("" ::"v"(wc[0]), "v"(wc[2]), "v"(fc[0]));
+}
+
 // Compute-wave loop over one unrolled round of NS stages x CC channels (so every LDS offset is
 // an instruction immediate inside one of NBASE 32 KiB windows; the launcher requires
-// C % (NS * CC) == 0).  Channel k: issue channel k+1's reads into the other buffer (after the
-// stage barrier when k+1 opens a stage), wait for k's reads, 36 FMAs.  The last channel reads
-// a stale slot (discarded) and meets the loader's closing barrier, so every round is the same
-// code.
+// C % (NS * CC) == 0).  Channel k: barrier when channel k+1 opens a stage, wait for k's reads,
+// then k+1's reads interleaved with k's FMAs.  The last channel reads a stale slot
+// (discarded) and meets the loader's closing barrier, so every round is the same code.
 template <class G, int K, int M = 0>
 __device__ __forceinline__ void compute_round(const uint32_t (&wa)[G::NBASE],
                                               const uint32_t (&fa)[G::NBASE], float (&acc)[9][8],
@@ -244,36 +319,9 @@ __device__ __forceinline__ void compute_round(const uint32_t (&wa)[G::NBASE],
     f32x4(&fc)[2] = (K & 1) ? fB : fA;
     f32x4(&wn)[6] = (K & 1) ? wA : wB;
     f32x4(&fn)[2] = (K & 1) ? fA : fB;
-    // M: measurement modes (launcher knob stream_abl >> 3): 1 no LDS reads, 2 no FMAs,
-    // 4 no barriers (only valid without DMA)
     if constexpr (NEXT % G::CC == 0 && !(M & 4)) __builtin_amdgcn_s_barrier();
     lgk_wait<0>(wc, fc);  // this channel's reads (issued during the previous channel's FMAs)
-    // the next channel's eight reads go out in pairs between the FMA chunks, so the LDS queue
-    // never holds a wave's whole batch while its FMAs wait to issue
-    const uint32_t w_ = wa[WIN], f_ = fa[WIN];
-    if constexpr (G::S2 == 2) {
-      if constexpr (!(M & 1)) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
-      if constexpr (!(M & 2)) fma_ti<2, 0, 2>(acc, wc, fc);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(M & 1)) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
-      if constexpr (!(M & 2)) fma_ti<2, 2, 4>(acc, wc, fc);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(M & 1)) read2<IMM + 64, IMM + 80>(w_, w_, wn[4], wn[5]);
-      if constexpr (!(M & 2)) fma_ti<2, 4, 6>(acc, wc, fc);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(M & 1)) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
-      if constexpr (!(M & 2)) fma_ti<2, 6, 9>(acc, wc, fc);
-    } else {
-      if constexpr (!(M & 1)) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
-      if constexpr (!(M & 2)) fma_ti<1, 0, 3>(acc, wc, fc);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(M & 1)) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
-      if constexpr (!(M & 2)) fma_ti<1, 3, 6>(acc, wc, fc);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(M & 1)) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
-      if constexpr (!(M & 2)) fma_ti<1, 6, 9>(acc, wc, fc);
-    }
-    if constexpr ((M & 2) != 0) asm volatile("" ::"v"(wc[0]), "v"(wc[5]), "v"(fc[1]));
+    channel_body<G, IMM, M>(wa[WIN], fa[WIN], acc, wc, fc, wn, fn);
     // keep this channel's FMAs between its wait and the next channel's (left alone, the
     // scheduler sinks them past later reads and the live ranges overflow into scratch)
     __builtin_amdgcn_sched_barrier(0);
@@ -281,11 +329,23 @@ __device__ __forceinline__ void compute_round(const uint32_t (&wa)[G::NBASE],
   }
 }
 
+template <class G, int M>
+__device__ __forceinline__ void compute_loop(int C, int nst, const uint32_t (&wa)[G::NBASE],
+                                             const uint32_t (&fa)[G::NBASE], float (&acc)[9][8],
+                                             f32x4 (&wA)[6], f32x4 (&fA)[2], f32x4 (&wB)[6],
+                                             f32x4 (&fB)[2]) {
+  for (int c0 = 0; c0 < C; c0 += G::NS * G::CC)
+    compute_round<G, 0, M>(wa, fa, acc, wA, fA, wB, fB);
+  if constexpr ((M & 4) != 0)
+    for (int k = 0; k < nst; ++k) __builtin_amdgcn_s_barrier();
+}
+
 template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
-    const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
-    int C, int H, int W, int Ho, int Wo, int nband, int ntx, int layout, float divisor,
-    float inv_divisor, OutEpi epi, int abl) {
+    const typename G::Elem* __restrict__ in1, const typename G::Elem* __restrict__ in2,
+    typename G::Elem* __restrict__ out, int C, int H, int W, int Ho, int Wo, int nband,
+    int ntx, int layout, float divisor, float inv_divisor, OutEpi epi, int abl) {
+  using T = typename G::Elem;
   static_assert((G::NS * G::CC) % 2 == 0, "buffer parity repeats every round");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // logical block = (n, row parity, band, column tile), tile fastest: the tiles and bands of
@@ -295,18 +355,18 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
   const int band = (t / ntx) % nband;
   const int py = (t / (ntx * nband)) % G::NPY;
   const int n = t / (ntx * nband * G::NPY);
-  const int Y0 = band * G::R;       // first (parity) row of the band
-  const int X04 = tx * G::TW4;      // first quad of the column tile
-  const int nst = C / G::CC;        // ring stages
-  const int W4 = W >> 2;
+  const int Y0 = band * G::R;         // first (parity) row of the band
+  const int X0Q = tx * G::TWQ;        // first quad of the column tile
+  const int nst = C / G::CC;          // ring stages
+  const int WQ = W / G::EPQ;          // image quads per row
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t plane = (uint32_t)(H * W);
-  const uint32_t plane_b = plane * 4u;
+  const uint32_t plane_b = plane * (uint32_t)sizeof(T);
   const uint32_t img_bytes = (uint32_t)C * plane_b;  // < 2^31 (launcher)
-  const float* img1 = in1 + (size_t)n * C * plane;
-  const float* img2 = in2 + (size_t)n * C * plane;
+  const T* img1 = in1 + (size_t)n * C * plane;
+  const T* img2 = in2 + (size_t)n * C * plane;
   const uint32_t lds0 = lds_addr(lds);
   if (wave == 0) CENSUS(0);
 
@@ -318,14 +378,14 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
     for (int i = 0; i < G::IPC; ++i) {
       const bool f2 = i < G::IF2;
       const int j = (f2 ? 64 * i : 64 * i - G::F2Q) + lane;
-      // slot quad q of LDS row rho holds image quad X04 - 2 + q (q < TW4 + 4; the last quad
-      // of a row is padding): halo quads come from the neighbouring tile or read zero
-      const int rho = j / G::S, q = j % G::S, cq = X04 - 2 + q;
+      // slot quad q of LDS row rho holds image quad X0Q - HQ + q (q < TWQ + 2 HQ; the rest of
+      // the row is padding): halo quads come from the neighbouring tile or read zero
+      const int rho = j / G::S, q = j % G::S, cq = X0Q - G::HQ + q;
       const int prow = f2 ? Y0 - 4 + rho : Y0 + rho;  // parity row (S2 = 2) or row
       const int srow = G::S2 == 2 ? 2 * prow + py : prow;
-      const bool ok = rho < (f2 ? G::F2R : G::R) && q < G::TW4 + 4 && cq >= 0 && cq < W4 &&
-                      prow >= 0 && srow < H;
-      rel[i] = ok ? (uint32_t)(srow * W + 4 * cq) * 4u : kOOB;
+      const bool ok = rho < (f2 ? G::F2R : G::R) && q < G::TWQ + 2 * G::HQ && cq >= 0 &&
+                      cq < WQ && prow >= 0 && srow < H;
+      rel[i] = ok ? (uint32_t)(srow * W + G::EPQ * cq) * (uint32_t)sizeof(T) : kOOB;
     }
     if (abl & 2) {  // measurement: no DMA (barriers only)
       for (int k = 0; k <= nst; ++k) __builtin_amdgcn_s_barrier();
@@ -363,13 +423,16 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
     const int r = useb ? rb : ra, tj = useb ? tb : ta;
     const int seg = blk * G::BS + (sp < G::BS ? sp : 0);
     const bool active = gi < G::NG && sp < G::BS && seg < G::NSEG && (p < 8 || hasb);
+    const int sg = seg < G::NSEG ? seg : 0;  // a duplicate address for idle lanes (broadcast)
+    // window: from pixel x0 - 4 S2, i.e. padded pixel 8 seg + 8 - 4 S2 (fp32: quad 2 seg or
+    // 2 seg + 1; fp16: quad seg, element 0 or 4); f1: padded pixel 8 seg + 8
+    const int wq = G::H16 ? sg : 2 * sg + (G::S2 == 2 ? 0 : 1);
+    const int fq = G::H16 ? sg + 1 : 2 * sg + 2;
     uint32_t wa[G::NBASE], fa[G::NBASE];
-    // window from column x0 - 4 S2: padded quad 2 seg (stride 2) or 2 seg + 1 (stride 1)
-    const int wq = 2 * seg + (G::S2 == 2 ? 0 : 1);
 #pragma unroll
     for (int k = 0; k < G::NBASE; ++k) {
       wa[k] = lds0 + (uint32_t)(k * 32768 + ((r + tj) * G::S + wq) * 16);
-      fa[k] = lds0 + (uint32_t)(k * 32768 + (G::F2Q + r * G::S + 2 * seg + 2) * 16);
+      fa[k] = lds0 + (uint32_t)(k * 32768 + (G::F2Q + r * G::S + fq) * 16);
     }
 
     float acc[9][8];
@@ -384,32 +447,21 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
       acc[0][0] = (float)C;
     } else {
       __builtin_amdgcn_s_barrier();  // B_0: stage 0 landed
-      read2<0, 16>(wa[0], wa[0], wA[0], wA[1]);
-      read2<32, 48>(wa[0], wa[0], wA[2], wA[3]);
-      read2<64, 80>(wa[0], wa[0], wA[4], wA[5]);
-      read2<0, 16>(fa[0], fa[0], fA[0], fA[1]);
-      const int mode = abl >> 3;
-      if (mode == 0) {
-        for (int c0 = 0; c0 < C; c0 += G::NS * G::CC)
-          compute_round<G, 0>(wa, fa, acc, wA, fA, wB, fB);
-      } else if (mode == 1) {
-        for (int c0 = 0; c0 < C; c0 += G::NS * G::CC)
-          compute_round<G, 0, 1>(wa, fa, acc, wA, fA, wB, fB);
-      } else if (mode == 2) {
-        for (int c0 = 0; c0 < C; c0 += G::NS * G::CC)
-          compute_round<G, 0, 2>(wa, fa, acc, wA, fA, wB, fB);
-      } else if (mode == 5) {
-        for (int c0 = 0; c0 < C; c0 += G::NS * G::CC)
-          compute_round<G, 0, 5>(wa, fa, acc, wA, fA, wB, fB);
-        for (int k = 0; k < nst; ++k) __builtin_amdgcn_s_barrier();
-      } else if (mode == 6) {
-        for (int c0 = 0; c0 < C; c0 += G::NS * G::CC)
-          compute_round<G, 0, 6>(wa, fa, acc, wA, fA, wB, fB);
-        for (int k = 0; k < nst; ++k) __builtin_amdgcn_s_barrier();
+      if constexpr (G::H16) {
+        read2<0, 16>(wa[0], wa[0], wA[0], wA[1]);
+        read2<32, 0>(wa[0], fa[0], wA[2], fA[0]);
       } else {
-        for (int c0 = 0; c0 < C; c0 += G::NS * G::CC)
-          compute_round<G, 0, 4>(wa, fa, acc, wA, fA, wB, fB);
-        for (int k = 0; k < nst; ++k) __builtin_amdgcn_s_barrier();
+        read2<0, 16>(wa[0], wa[0], wA[0], wA[1]);
+        read2<32, 48>(wa[0], wa[0], wA[2], wA[3]);
+        if constexpr (G::S2 == 2) read2<64, 80>(wa[0], wa[0], wA[4], wA[5]);
+        read2<0, 16>(fa[0], fa[0], fA[0], fA[1]);
+      }
+      switch (abl >> 3) {
+        case 0: compute_loop<G, 0>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        case 1: compute_loop<G, 1>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        case 2: compute_loop<G, 2>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        case 5: compute_loop<G, 5>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        default: compute_loop<G, 6>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
       }
       lgk_wait<0>(wA, fA);  // the last (discarded) reads
     }
@@ -420,7 +472,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
     if (wave == 0) CENSUS(5);  // past the park barrier
     if (active) {
       // out = acc / C (cu:100): an exact multiply when C is a power of two (a uniform branch,
-      // so the IEEE division sequence is not evaluated and discarded per value)
+      // so the division sequence is not evaluated and discarded per value)
       if (inv_divisor != 0.f) {
 #pragma unroll
         for (int ti = 0; ti < 9; ++ti)
@@ -442,43 +494,59 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
 #pragma unroll
       for (int ti = 0; ti < 9; ++ti) {
         const int oc = out_channel(layout, tj - 4, ti - 4, 4, 9, G::S2);
+        f32x4* prow = reinterpret_cast<f32x4*>(lds) + (oc * G::R + r) * G::PRQ;
+        if constexpr (G::H16) {
+          // one quad per lane; odd segment blocks XOR 4 so the two blocks sharing a
+          // ds_write_b128 lane group (8 consecutive lanes) hit disjoint 16-B slots
+          f16x8 v;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          f32x4 v;
+          for (int e = 0; e < 8; ++e) v[e] = (_Float16)epi_act(acc[ti][e], epi.slope);  // :84
+          prow[seg ^ (4 * (blk & 1))] = __builtin_bit_cast(f32x4, v);
+        } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = epi_act(acc[ti][4 * h + e], epi.slope);  // :84
-          // odd segment blocks swap their two quads: the two blocks sharing a ds_write_b128
-          // lane group (8 consecutive lanes) then hit disjoint 16-B slots
-          const int pq = 2 * seg + (h ^ (blk & 1));
-          *reinterpret_cast<f32x4*>(lds + ((oc * G::R + r) * G::TW4 + pq) * 4) = v;
+          for (int h = 0; h < 2; ++h) {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = epi_act(acc[ti][4 * h + e], epi.slope);  // :84
+            // odd segment blocks swap their two quads: the two blocks sharing a
+            // ds_write_b128 lane group then hit disjoint 16-B slots
+            prow[2 * seg + (h ^ (blk & 1))] = v;
+          }
         }
       }
     }
   }
   if (wave == G::NWC) __builtin_amdgcn_s_barrier();  // the loader's side of the park barrier
   __syncthreads();
-  // ---------------- epilogue: whole output rows, every wave, nontemporal ----------------
+  // ---------------- epilogue: whole output row segments, every wave, nontemporal ----------
   if (wave == 0) CENSUS(3);  // parked
   if (abl & 4) return;  // measurement: no stores
-  float* oimg = out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * Ho * Wo);
-  constexpr int NQ = 81 * G::R * G::TW4;
+  T* oimg = out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * Ho * Wo);
+  constexpr int NQ = 81 * G::R * G::TWQ;
   constexpr int PER = (NQ + G::THREADS - 1) / G::THREADS;
   st_f32x4 v[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {  // all LDS reads first, then all stores
     const int q = threadIdx.x + i * G::THREADS;
-    const int xq = q % G::TW4, seg = xq >> 1;
-    const int pq = q - xq + 2 * seg + ((xq & 1) ^ ((seg / G::BS) & 1));  // park swizzle
+    const int row = q / G::TWQ, xq = q - row * G::TWQ;
+    int pq;
+    if constexpr (G::H16) {
+      pq = row * G::PRQ + (xq ^ (4 * ((xq / G::BS) & 1)));
+    } else {
+      const int seg = xq >> 1;
+      pq = row * G::PRQ + 2 * seg + ((xq & 1) ^ ((seg / G::BS) & 1));
+    }
     if (q < NQ) v[i] = *reinterpret_cast<const st_f32x4*>(lds + 4 * pq);
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int q = threadIdx.x + i * G::THREADS;
-    const int oc = q / (G::R * G::TW4);
-    const int rem = q - oc * (G::R * G::TW4);
-    const int r = rem / G::TW4, xq = X04 + rem - r * G::TW4;
+    const int oc = q / (G::R * G::TWQ);
+    const int rem = q - oc * (G::R * G::TWQ);
+    const int r = rem / G::TWQ, xq = X0Q + rem - r * G::TWQ;
     const int y = G::S2 == 2 ? 2 * (Y0 + r) + py : Y0 + r;
-    if (q < NQ && y < Ho && xq < W4) st_out4(oimg + ((size_t)oc * Ho + y) * Wo + 4 * xq, v[i]);
+    if (q < NQ && y < Ho && xq < WQ)
+      st_out4(reinterpret_cast<float*>(oimg + ((size_t)oc * Ho + y) * Wo + G::EPQ * xq), v[i]);
   }
   if (wave == 0) CENSUS(4);  // stores issued
 }
@@ -486,9 +554,10 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
 template <class G>
 static hipError_t launch(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
                          int layout, float divisor, hipStream_t stream) {
+  using T = typename G::Elem;
   const int HP = G::S2 == 2 ? (H + 1) / 2 : H;  // (parity) rows; parity 0 has the extra row
   const int nband = (HP + G::R - 1) / G::R;
-  const int ntx = (W / 4 + G::TW4 - 1) / G::TW4;
+  const int ntx = (W + G::TWP - 1) / G::TWP;
   const long long nblk = (long long)B * G::NPY * nband * ntx;
   if (nblk <= 0) return hipSuccess;
   if (C <= 0 || C % (G::NS * G::CC)) return hipErrorNotSupported;  // whole unrolled rounds
@@ -507,19 +576,18 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
   hipExtLaunchKernelGGL((corr_fwd_stream<G>), dim3((unsigned)nblk), dim3(G::THREADS),
-                        G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,
-                        (float*)out, C, H, W, H, W, nband, ntx, layout, divisor, inv,
-                        current_epi(), debug_knob("stream_abl", 0));
+                        G::LDS_BYTES, stream, ev0, ev1, 0, (const T*)in1, (const T*)in2,
+                        (T*)out, C, H, W, H, W, nband, ntx, layout, divisor, inv, current_epi(),
+                        debug_knob("stream_abl", 0));
   return hipGetLastError();
 }
 
-template <int S2, int TW4>
+template <typename T, int S2, int TWP>
 static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
                        int layout, float divisor, hipStream_t stream) {
-  switch (debug_knob("stream_cfg", 0)) {  // measurement variants (R, CC, NS)
-    case 1: return launch<Geo<S2, 3, TW4, 1, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    case 2: return launch<Geo<S2, 3, TW4, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    default: return launch<Geo<S2, 3, TW4, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+  switch (debug_knob("stream_cfg", 0)) {  // measurement variants (CC, NS)
+    case 2: return launch<Geo<T, S2, 3, TWP, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+    default: return launch<Geo<T, S2, 3, TWP, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
   }
 }
 
@@ -528,26 +596,35 @@ static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C
 // hipErrorNotSupported: a shape this kernel does not serve (the caller tries the next path).
 // Serves k = 1, s1 = 1, pad = md (output = input size) with dr = 4: s2 = 2 (model.py:24's
 // Correlation(9,1,9,1,2)) or s2 = 1 (Correlation(4,1,4,1,1), CostVolumeLayer(sr=4) with the
-// CVL channel order); fp32; W % 4 == 0 and 16-B aligned pointers; C a multiple of 16; grids of
-// at least ~one workgroup per CU (smaller grids have faster homes: corr_pt / corr_rows).
-hipError_t corr_forward_stream_f32(const void* in1, const void* in2, void* out, int B, int C,
-                                   int H, int W, int s2, int layout, float divisor,
-                                   hipStream_t stream) {
-  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16 || W % 4)
+// CVL channel order); fp32 or fp16 storage (dtype 0 / 1); W a multiple of 4 (fp32) or 8
+// (fp16) and 16-B aligned pointers; C a multiple of 16; grids of at least ~one workgroup per
+// CU (smaller grids have faster homes: corr_pt / corr_rows).
+hipError_t corr_forward_stream(const void* in1, const void* in2, void* out, int B, int C, int H,
+                               int W, int s2, int dtype, int layout, float divisor,
+                               hipStream_t stream) {
+  const int epq = dtype == 1 ? 8 : 4;
+  if (dtype != 0 && dtype != 1) return hipErrorNotSupported;
+  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16 || W % epq)
     return hipErrorNotSupported;
-  if ((size_t)C * H * W * 4 >= 0x7ffffff0ull || C % 16) return hipErrorNotSupported;
-  const int W4 = W / 4;
-  const int tw4 = (W4 % 28 == 0 || W4 < 28) ? 28 : 32;  // 112- or 128-pixel column tiles
+  if ((size_t)C * H * W * (16 / epq) >= 0x7ffffff0ull || C % 16) return hipErrorNotSupported;
+  const int twp = (W % 112 == 0 || W < 112) ? 112 : 128;  // column tile width in pixels
   const long long nblk = (long long)B * (s2 == 2 ? 2 : 1) *
-                         (((s2 == 2 ? (H + 1) / 2 : H) + 2) / 3) * ((W4 + tw4 - 1) / tw4);
-  if (nblk < 192 || W4 < 16) return hipErrorNotSupported;
+                         (((s2 == 2 ? (H + 1) / 2 : H) + 2) / 3) * ((W + twp - 1) / twp);
+  if (nblk < 192 || W < 64) return hipErrorNotSupported;
   using namespace stream;
-  if (s2 == 2)
-    return tw4 == 28 ? pick<2, 28>(in1, in2, out, B, C, H, W, layout, divisor, stream)
-                     : pick<2, 32>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-  if (s2 == 1)
-    return tw4 == 28 ? pick<1, 28>(in1, in2, out, B, C, H, W, layout, divisor, stream)
-                     : pick<1, 32>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+#define PWC_PICK(T)                                                                            \
+  if (s2 == 2)                                                                                 \
+    return twp == 112 ? pick<T, 2, 112>(in1, in2, out, B, C, H, W, layout, divisor, stream)    \
+                      : pick<T, 2, 128>(in1, in2, out, B, C, H, W, layout, divisor, stream);   \
+  if (s2 == 1)                                                                                 \
+    return twp == 112 ? pick<T, 1, 112>(in1, in2, out, B, C, H, W, layout, divisor, stream)    \
+                      : pick<T, 1, 128>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+  if (dtype == 0) {
+    PWC_PICK(float)
+  } else {
+    PWC_PICK(__half)
+  }
+#undef PWC_PICK
   return hipErrorNotSupported;
 }
 

@@ -67,7 +67,7 @@ int main(int argc, char** argv) {
   for (int i = 0; i < 10; ++i) {
     unsigned long long* p = cen;
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::stream::g_census), &p, sizeof(p)));
-    CK(pwc::corr_forward_stream_f32(f1[i % NS], f2[i % NS], out[i % NS], B, C, H, W, 2, 0, 32.f, 0));
+    CK(pwc::corr_forward_stream(f1[i % NS], f2[i % NS], out[i % NS], B, C, H, W, 2, 0, 0, 32.f, 0));
   }
   CK(hipDeviceSynchronize());
   for (int i = 0; i < iters; ++i) {
@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::stream::g_census), &p, sizeof(p)));
     pwc::g_e0 = e0[i];
     pwc::g_e1 = e1[i];
-    CK(pwc::corr_forward_stream_f32(f1[i % NS], f2[i % NS], out[i % NS], B, C, H, W, 2, 0, 32.f, 0));
+    CK(pwc::corr_forward_stream(f1[i % NS], f2[i % NS], out[i % NS], B, C, H, W, 2, 0, 0, 32.f, 0));
   }
   CK(hipDeviceSynchronize());
   std::vector<unsigned long long> c((size_t)iters * nblk * 8);
