@@ -25,7 +25,7 @@ def mean_kb(path, sub):
 
 def main():
     fetch, write, out = sys.argv[1:4]
-    sub = sys.argv[4] if len(sys.argv) > 4 else "corr_fwd_pt"
+    sub = sys.argv[4] if len(sys.argv) > 4 else "corr_fwd_stream"
     f, n, name = mean_kb(fetch, sub)
     w, _, _ = mean_kb(write, sub)
     rd = int(f * 1024 * 2)
@@ -46,7 +46,7 @@ def main():
         "traffic_over_algorithmic": round((rd + wr) / ALG, 4),
         "collected_with": "rocprofv3 --pmc FETCH_SIZE (and separately WRITE_SIZE) "
                           f"--kernel-include-regex {sub} -- python tools/kbench.py --levels 4 "
-                          "--iters 20 (tools/profile_round.sh)",
+                          "--ops corr --iters 20 (tools/gpu_profile_r02.sh)",
     }
     json.dump(d, open(out, "w"), indent=1)
     print(json.dumps(d))
