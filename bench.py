@@ -17,9 +17,13 @@ broadcasts the Net harness's weights (pwcnet_amd/net.py; SURVEY §8e's startup b
 every rank checks it received them.
 
 Timed region: every step replays the hipGraph of its buffer set (warp + correlation at l0..l3
-and the l4 warp) and then launches the l4 correlation -- the dominant kernel, priced for the
-roofline -- through the C ABI with hipExtLaunchKernel start/stop events (pwc_time_next_corr),
-so that kernel's duration is measured live in every timed step on the stream it runs on.
+and the l4 warp, all direct C-ABI calls on buffers bound once per set) and then launches the
+l4 correlation -- the dominant kernel, priced for the roofline -- through the C ABI with
+hipExtLaunchKernel start/stop events (pwc_time_next_corr), so that kernel's duration is
+measured live in every timed step on the stream it runs on.  (HIP refuses external
+event-record nodes in a capture, so a captured l4 launch could not carry events; the
+comparison mode ``--timing graph-all`` captures the whole step in one graph, without kernel
+events: it measures the eager launch's share of the step.)
 Inputs rotate over enough buffer sets (> 2x the 256 MiB Infinity Cache) that each step reads
 them from HBM.  After timing, a replay self-check re-runs one step with every output poisoned
 (NaN) and compares all five levels bit for bit with a fresh eager computation, and a shard
@@ -96,7 +100,11 @@ def parse_args(argv=None):
     ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches (timing 'eager')")
+    ap.add_argument("--timing", default="graph-eager", choices=["graph-eager", "graph-all"],
+                    help="graph-eager: per-set graphs of l0..l3 + the l4 warp, then an eager "
+                         "event-armed l4 correlation; graph-all (comparison only): the whole "
+                         "step in one graph, no kernel events")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = launcher rehearsal over gloo with a torch-CPU stand-in op")
     ap.add_argument("--fused-levels", default="0,1",
@@ -169,45 +177,85 @@ class HipPass:
     """warp + Correlation(model.py:24) at l0..l4 through pwcnet_amd (C ABI); the l4
     correlation is a direct, pre-bound C-ABI call so it can carry the timing events."""
 
+    P = (CORR_ARGS["pad_size"], CORR_ARGS["kernel_size"], CORR_ARGS["max_displacement"],
+         CORR_ARGS["stride1"], CORR_ARGS["stride2"])
+
     def __init__(self, dev, dtype, fused):
         from pwcnet_amd import _lib
-        from pwcnet_amd.ops import corr_forward, warp_corr_forward, warp_forward
+        from pwcnet_amd.ops import corr_forward, warp_forward
         self._lib = _lib
         self.lib = _lib.load()  # raises if the HIP library is missing: there is no fallback
         self.warp_forward, self.corr_forward = warp_forward, corr_forward
-        self.warp_corr_forward = warp_corr_forward
         self.dev, self.dtype, self.fused = dev, dtype, fused
-        self.stream = torch.cuda.current_stream(dev)
-        self.sp = ctypes.c_void_p(self.stream.cuda_stream)
         self.dcode = _lib.DTYPE_CODES[dtype]
+
+    def bind(self, s):
+        """Allocate every level's outputs (x2_warp, the volume) and split-channel workspace
+        once, outside any capture, so the per-step graphs only hold kernel nodes."""
+        L, P = self.lib, self.P
+        for l, lv in enumerate(s):
+            B, C, h, w = lv["x1"].shape
+            OC, Ho, Wo = self._lib.corr_output_shape(h, w, *P)
+            lv["x2w"] = torch.empty_like(lv["x2"])
+            lv["corr"] = torch.empty((B, OC, Ho, Wo), dtype=self.dtype, device=self.dev)
+            nws = (L.pwc_warp_corr_workspace_size(B, C, h, w, *P, self.dcode, 1)
+                   if l in self.fused else L.pwc_corr_workspace_size(B, C, h, w, *P))
+            lv["ws"] = torch.empty(max(int(nws), 1), dtype=torch.uint8, device=self.dev)
+            lv["nws"] = int(nws)
+
+    @property
+    def sp(self):
+        """The CURRENT stream (torch.cuda.graph captures on its own side stream)."""
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    @staticmethod
+    def _p(t):
+        return ctypes.c_void_p(t.data_ptr())
 
     def pre(self, s):
         """l0..l3 (warp + corr; fused levels as one WarpCorrelation launch that also emits
-        x2_warp) and the l4 warp; the l4 warped features land in s[-1]["x2w"]."""
+        x2_warp) and the l4 warp, all direct C-ABI calls on the bound buffers."""
+        L, P, p = self.lib, self.P, self._p
         for l, lv in enumerate(s[:-1]):
+            B, C, h, w = lv["x1"].shape
             if l in self.fused:
-                lv["corr"], lv["x2w"] = self.warp_corr_forward(lv["x1"], lv["x2"], lv["flow"],
-                                                               **CORR_ARGS)
+                ret = L.pwc_warp_corr_forward(p(lv["x1"]), p(lv["x2"]), p(lv["flow"]),
+                                              p(lv["x2w"]), p(lv["corr"]), B, C, h, w, *P, 1,
+                                              self.dcode, p(lv["ws"]), lv["nws"], self.sp)
             else:
-                lv["x2w"] = self.warp_forward(lv["x2"], lv["flow"])
-                lv["corr"] = self.corr_forward(lv["x1"], lv["x2w"], **CORR_ARGS)
-        s[-1]["x2w"] = self.warp_forward(s[-1]["x2"], s[-1]["flow"])
+                ret = L.pwc_warp_forward(p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]), B, C, h, w,
+                                         self.dcode, self.sp)
+                if ret == 1:
+                    ret = L.pwc_corr_forward_ws(p(lv["x1"]), p(lv["x2w"]), p(lv["corr"]), B, C,
+                                                h, w, *P, 1, self.dcode, p(lv["ws"]), lv["nws"],
+                                                self.sp)
+            if ret != 1:
+                self._lib.check(ret, f"bench level {l}")
+        lv = s[-1]
+        B, C, h, w = lv["x1"].shape
+        ret = L.pwc_warp_forward(p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]), B, C, h, w,
+                                 self.dcode, self.sp)
+        if ret != 1:
+            self._lib.check(ret, "bench l4 warp")
 
     def corr_l4(self, s, events=None):
+        """The l4 correlation; ``events`` (eager timing only) arms hipExtLaunchKernel's
+        start/stop events for this one launch -- never during a capture."""
         lv = s[-1]
         B, C, h, w = lv["x1"].shape
         if events is not None:
             self._lib.check(self.lib.pwc_time_next_corr(ctypes.c_void_p(events[0].cuda_event),
                                                         ctypes.c_void_p(events[1].cuda_event)),
                             "bench")
-        ret = self.lib.pwc_corr_forward(ctypes.c_void_p(lv["x1"].data_ptr()),
-                                        ctypes.c_void_p(lv["x2w"].data_ptr()),
-                                        ctypes.c_void_p(lv["corr"].data_ptr()), B, C, h, w,
-                                        9, 1, 9, 1, 2, 1, self.dcode, self.sp)
+        ret = self.lib.pwc_corr_forward(self._p(lv["x1"]), self._p(lv["x2w"]),
+                                        self._p(lv["corr"]), B, C, h, w, *self.P, 1, self.dcode,
+                                        self.sp)
         if ret != 1:
             self._lib.check(ret, "bench corr_l4")
 
     def full(self, s):
+        if "ws" not in s[0]:
+            self.bind(s)
         self.pre(s)
         self.corr_l4(s)
 
@@ -477,32 +525,47 @@ def main(argv=None):
         sets = [random_set(shapes, B, dev, dtype, gen) for _ in range(nsets)]
 
     graphs = []
+    timing = "cpu" if cpu else ("eager" if args.no_graph else args.timing)
     if not cpu:
+        for s in sets:
+            pass_.bind(s)
         for s in sets:  # first calls (kernel attributes) outside any capture
             pass_.full(s)
         torch.cuda.synchronize(dev)
-        if not args.no_graph:
-            # one hipGraph per buffer set: warp + corr at l0..l3 and the l4 warp.  The l4
-            # correlation stays an eager launch after the replay so its start/stop events are
-            # real per-step measurements (an event-armed launch must never be captured).
-            pool = torch.cuda.graph_pool_handle()
-            for s in sets:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    pass_.pre(s)
-                graphs.append(g)
-            torch.cuda.synchronize(dev)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(args.steps)]
         for a, b in evs:  # materialise the hipEvent_t handles (torch creates them lazily)
             a.record()
             b.record()
         torch.cuda.synchronize(dev)
+        if timing == "graph-all":
+            # comparison mode: one hipGraph per buffer set with the WHOLE step (l4 correlation
+            # included); no per-kernel events (roofline timing is absent in this mode)
+            pool = torch.cuda.graph_pool_handle()
+            for s in sets:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    pass_.pre(s)
+                    pass_.corr_l4(s)
+                graphs.append(g)
+        elif timing == "graph-eager":
+            # one hipGraph per buffer set for l0..l3 and the l4 warp; the l4 correlation is an
+            # eager launch after the replay with hipExtLaunchKernel start/stop events
+            pool = torch.cuda.graph_pool_handle()
+            for s in sets:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    pass_.pre(s)
+                graphs.append(g)
+        torch.cuda.synchronize(dev)
 
     def step(i, ev=None):
         s = sets[i % nsets]
         if cpu:
             pass_.full(s)
+            return
+        if timing == "graph-all":
+            graphs[i % nsets].replay()
             return
         if graphs:
             graphs[i % nsets].replay()
@@ -575,13 +638,14 @@ def main(argv=None):
             "buffer_sets": nsets,
             "fused_levels": sorted(fused),
             "graph": bool(graphs),
+            "timing": timing,
             "device": "cpu (launcher rehearsal: torch-CPU stand-in, not the product path)"
                       if cpu else "cuda",
         },
         "checks": {"replay": replay_ok, "replay_max_rel_diff": replay_diff, "shards": shards,
                    "weights_broadcast": bcast},
     }
-    if not cpu:
+    if not cpu and timing != "graph-all":
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
         bytes_launch = corr_bytes_per_pair(C4, h4, w4, esz) * B
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
@@ -589,7 +653,7 @@ def main(argv=None):
                          and (args.height, args.width) == (384, 448) else (None, None))
         result["roofline"] = {
             "kernel": f"l4 correlation ({C4}x{h4}x{w4}, B={B}, {args.dtype}), start/stop events "
-                      "per timed step",
+                      f"per timed step ({'hipExtLaunchKernel start/stop events'})",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,

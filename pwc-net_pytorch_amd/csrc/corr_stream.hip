@@ -585,9 +585,15 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
 template <typename T, int S2, int TWP>
 static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C, int H, int W,
                        int layout, float divisor, hipStream_t stream) {
+  // ring: CC channels per stage x NS stages.  4 x 4 (half the barriers per channel) measured
+  // best or equal at every shape served in back-to-back launches (config-2 l4 fp32 19.6 ->
+  // 17.2 us against 2 x 8; Corr4, Sintel fp32/fp16 l3/l4; profiles/r02d_stream_ring_sweep.txt),
+  // where one launch's store tail overlaps the next one's loop; inside the bench step, where
+  // it cannot, all three rings measure the same 19.1-19.4 us (profiles/r02d_bench_ring_ab.txt)
   switch (debug_knob("stream_cfg", 0)) {  // measurement variants (CC, NS)
     case 2: return launch<Geo<T, S2, 3, TWP, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    default: return launch<Geo<T, S2, 3, TWP, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+    case 8: return launch<Geo<T, S2, 3, TWP, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+    default: return launch<Geo<T, S2, 3, TWP, 4, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
   }
 }
 
