@@ -512,8 +512,8 @@ static int band_mode() { return debug_knob("corr_band", 1); }
 hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                               int, float, int, hipStream_t);
 
-hipError_t corr_forward_rows_f32(const void*, const void*, void*, int, int, int, int, float,
-                                 hipStream_t);
+hipError_t corr_forward_rows(const void*, const void*, void*, int, int, int, int, float, int,
+                             hipStream_t);
 
 // corr_stream.hip: full-width row bands + loader wave (the l4-sized grids; it decides).
 hipError_t corr_forward_stream(const void*, const void*, void*, int, int, int, int, int, int,
@@ -553,10 +553,11 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
         warp_corr_band_f32(in1, in2, nullptr, nullptr, out, B, C, H, W, divisor, 0, stream);
     if (e != hipErrorNotSupported) return e;
   }
-  if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && layout == kRaster &&
-      s2 == 2 && pad == md && (md == 8 || md == 9) &&
+  if (force_generic == 0 && k == 1 && s1 == 1 && (sizeof(T) == 4 || kHalf) &&
+      layout == kRaster && s2 == 2 && pad == md && (md == 8 || md == 9) &&
       (uintptr_t)in1 % 16 == 0 && (uintptr_t)in2 % 16 == 0 && (uintptr_t)out % 16 == 0) {
-    const hipError_t e = corr_forward_rows_f32(in1, in2, out, B, C, H, W, divisor, stream);
+    const hipError_t e =
+        corr_forward_rows(in1, in2, out, B, C, H, W, divisor, kHalf ? 1 : 0, stream);
     if (e != hipErrorNotSupported) return e;
   }
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4) {

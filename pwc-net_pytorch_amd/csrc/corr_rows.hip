@@ -1,5 +1,7 @@
 // corr_rows.hip — correlation forward of model.py:24's configuration (pad == md in {8, 9},
-// k 1, s1 1, s2 2: 81 displacement channels, /C) for the larger pyramid levels, fp32, W % 4 == 0.
+// k 1, s1 1, s2 2: 81 displacement channels, /C) for the mid-sized pyramid levels; fp32
+// storage (W % 4 == 0) or fp16 storage (W % 8 == 0: halves widened to fp32 on the way into
+// LDS, fp32 arithmetic, fp16 stores -- BASELINE config 4's coarse Sintel levels).
 //
 //   out[n, tj*9+ti, y, x] = sum_c f1[n,c,y,x] * f2[n,c,y+2tj-8,x+2ti-8] / C, zeros outside
 //   (correlation_cuda_kernel.cu:34-106 with kernel_size 1, stride1 1, stride2 2).
@@ -60,12 +62,18 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int R, int NT, int ML1, int ML2>
-__global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__ f1,
-                                                       const float* __restrict__ f2,
-                                                       float* __restrict__ out, int C, int H,
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+template <typename T, int R, int NT, int ML1, int ML2>
+__global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
+                                                       const T* __restrict__ f2,
+                                                       T* __restrict__ out, int C, int H,
                                                        int W, float divisor, float inv_divisor,
                                                        Geo g, OutEpi epi) {
+  constexpr bool H16 = sizeof(T) == 2;
+  constexpr int EPQ = 16 / (int)sizeof(T);  // pixels per 16-B quad
+  constexpr int HPQ = EPQ / 2;              // parity slots per quad and column parity
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NR2 = R + 8;
   const int t = threadIdx.x;
@@ -75,7 +83,7 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
   const int hp = (H - p + 1) >> 1;
   const int r0 = b * R;
   const uint32_t plane = (uint32_t)(H * W);
-  const uint32_t img_bytes = (uint32_t)C * plane * 4u;
+  const uint32_t img_bytes = (uint32_t)C * plane * (uint32_t)sizeof(T);
   const size_t img = (size_t)n * C * plane;
   const __amdgpu_buffer_rsrc_t rs1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(f1 + img), (short)0, (int)img_bytes, 0x00020000);
@@ -110,8 +118,10 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
     const int rest = qdiv(itm, g.inv_Q), qd = itm - rest * g.Q;
     const int c = rest / R, rho = rest - c * R;
     const bool ok = itm < tot1 && r0 + rho < hp;
-    vo1[j] = ok ? ((uint32_t)c * plane + (uint32_t)(2 * (r0 + rho) + p) * W + 4 * qd) * 4u : kOOB;
-    ld1[j] = itm < tot1 ? ((c * R + rho) * 2) * g.Wq4 + 2 * qd : -1;
+    vo1[j] = ok ? ((uint32_t)c * plane + (uint32_t)(2 * (r0 + rho) + p) * W + EPQ * qd) *
+                      (uint32_t)sizeof(T)
+                : kOOB;
+    ld1[j] = itm < tot1 ? ((c * R + rho) * 2) * g.Wq4 + HPQ * qd : -1;
     ch1[j] = c;
   }
 #pragma unroll
@@ -121,8 +131,10 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
     const int c = qdiv(rest, g.inv_NR2), k = rest - c * NR2;
     const int rr = r0 - 4 + k;
     const bool ok = itm < tot2 && rr >= 0 && rr < hp;
-    vo2[j] = ok ? ((uint32_t)c * plane + (uint32_t)(2 * rr + p) * W + 4 * qd) * 4u : kOOB;
-    ld2[j] = itm < tot2 ? g.f1f + ((c * NR2 + k) * 2) * g.Wf + 4 + 2 * qd : -1;
+    vo2[j] = ok ? ((uint32_t)c * plane + (uint32_t)(2 * rr + p) * W + EPQ * qd) *
+                      (uint32_t)sizeof(T)
+                : kOOB;
+    ld2[j] = itm < tot2 ? g.f1f + ((c * NR2 + k) * 2) * g.Wf + 4 + HPQ * qd : -1;
     ch2[j] = c;
   }
 
@@ -148,7 +160,7 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
   f32x4 v1[ML1], v2[ML2];
   auto issue = [&](int cb) {
     const int cn = min(g.ck, C - cb);
-    const int so = (int)((uint32_t)cb * plane * 4u);
+    const int so = (int)((uint32_t)cb * plane * (uint32_t)sizeof(T));
 #pragma unroll
     for (int j = 0; j < ML1; ++j)  // channels past C (last chunk) read zeros: range check
       v1[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -162,18 +174,25 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
   for (int cb = 0; cb < C; cb += g.ck) {
     const int cn = min(g.ck, C - cb);
     if (cb > 0) lds_barrier();  // the previous chunk's compute is done with the staging
+    // split into column parities (fp16: widened to fp32 here)
+    auto put = [&](int dst, int half, const f32x4& v) {
+      if constexpr (H16) {
+        const f16x8 h = __builtin_bit_cast(f16x8, v);
+        *reinterpret_cast<f32x4*>(lds + dst) =
+            f32x4{(float)h[0], (float)h[2], (float)h[4], (float)h[6]};
+        *reinterpret_cast<f32x4*>(lds + dst + half) =
+            f32x4{(float)h[1], (float)h[3], (float)h[5], (float)h[7]};
+      } else {
+        *reinterpret_cast<f32x2*>(lds + dst) = f32x2{v.x, v.z};
+        *reinterpret_cast<f32x2*>(lds + dst + half) = f32x2{v.y, v.w};
+      }
+    };
 #pragma unroll
-    for (int j = 0; j < ML1; ++j) {
-      if (ld1[j] < 0) continue;
-      *reinterpret_cast<f32x2*>(lds + ld1[j]) = f32x2{v1[j].x, v1[j].z};
-      *reinterpret_cast<f32x2*>(lds + ld1[j] + g.Wq4) = f32x2{v1[j].y, v1[j].w};
-    }
+    for (int j = 0; j < ML1; ++j)
+      if (ld1[j] >= 0) put(ld1[j], g.Wq4, v1[j]);
 #pragma unroll
-    for (int j = 0; j < ML2; ++j) {
-      if (ld2[j] < 0) continue;
-      *reinterpret_cast<f32x2*>(lds + ld2[j]) = f32x2{v2[j].x, v2[j].z};
-      *reinterpret_cast<f32x2*>(lds + ld2[j] + g.Wf) = f32x2{v2[j].y, v2[j].w};
-    }
+    for (int j = 0; j < ML2; ++j)
+      if (ld2[j] >= 0) put(ld2[j], g.Wf, v2[j]);
     if (cb + g.ck < C) issue(cb + g.ck);
     lds_barrier();
     if (active) {
@@ -234,7 +253,12 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
     v4 = f32x4{epi_act(v4.x, epi.slope), epi_act(v4.y, epi.slope), epi_act(v4.z, epi.slope),
                epi_act(v4.w, epi.slope)};
     const size_t ib = epi.ostride ? (size_t)n * epi.ostride : (size_t)n * (D * D) * H * W;
-    st_out4(out + ib + ((size_t)(tj * D + ti) * H + (2 * row + p)) * W + 4 * m, v4);
+    T* dst = out + ib + ((size_t)(tj * D + ti) * H + (2 * row + p)) * W + 4 * m;
+    if constexpr (H16)
+      *reinterpret_cast<f16x4*>(dst) =
+          f16x4{(_Float16)v4.x, (_Float16)v4.y, (_Float16)v4.z, (_Float16)v4.w};
+    else
+      st_out4(dst, v4);
   }
 }
 
@@ -243,12 +267,15 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const float* __restrict__
 // Serves l3-sized grids (13..24 parity rows per image) by default.  PWC_ROWS=0 disables the
 // kernel, PWC_ROWS=1 selects it at every size >= 13 parity rows, PWC_ROWS_CFG="R,CK" forces
 // a configuration at any size (measurement).
-hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, int B, int C,
-                                 int H, int W, float divisor, hipStream_t stream) {
+// dtype 0: fp32 storage, 1: fp16 (Sintel l0..l2 of config 4: every parity-row count, W % 8).
+hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B, int C, int H,
+                             int W, float divisor, int dtype, hipStream_t stream) {
   using namespace rows;
   const int mode = debug_knob("rows", 1);  // 0 off, 2 forced at every size (measurement)
-  if (mode == 0) return hipErrorNotSupported;
-  if (W % 4 != 0 || W < 8 || B == 0) return hipErrorNotSupported;
+  if (mode == 0 || (dtype != 0 && dtype != 1)) return hipErrorNotSupported;
+  const bool h16 = dtype == 1;
+  const int epq = h16 ? 8 : 4;
+  if (W % epq != 0 || W < 8 || B == 0) return hipErrorNotSupported;
   if ((size_t)B * C * H * W >= (1ull << 30) || (size_t)B * 81 * H * W >= (1ull << 31))
     return hipErrorNotSupported;
   // measured (tools/gpu_rows.sh, B=8 384x448): l2 (12 parity rows) stays on corr_pt.hip,
@@ -258,6 +285,9 @@ hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, in
   if (debug_knob("rows_r", 0) > 0) {
     R = debug_knob("rows_r", R);
     CK = debug_knob("rows_ck", CK);
+  } else if (h16) {
+    R = hp0 <= 12 ? 1 : R;  // fp16 has no parity-tile / band kernel for the small levels
+    if (hp0 > 24 && mode != 2) return hipErrorNotSupported;
   } else if (hp0 <= 12 || (hp0 > 24 && mode != 2)) {
     return hipErrorNotSupported;
   }
@@ -265,7 +295,7 @@ hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, in
   g.Wq4 = ((W / 2) + 3) & ~3;
   g.Wf = g.Wq4 + 8;
   g.S = g.Wq4 / 4;
-  g.Q = W / 4;
+  g.Q = W / epq;
   g.I = D * R * 2 * g.S;
   constexpr int NT = 768;
   if (g.I > NT || R < 1) return hipErrorNotSupported;
@@ -281,7 +311,7 @@ hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, in
   const size_t red = (size_t)g.G * g.I * D * 16;
   const size_t lds = stage > red ? stage : red;
   if (lds > 160 * 1024) return hipErrorNotSupported;
-  const int per1 = (g.ck * R * g.Q + NT - 1) / NT;
+  const int per1 = (g.ck * R * g.Q + NT - 1) / NT;  // 16-B loads per thread per chunk
   const int per2 = (g.ck * (R + 8) * g.Q + NT - 1) / NT;
   g.inv_Q = 1.f / (float)g.Q;
   g.inv_NR2 = 1.f / (float)(R + 8);
@@ -293,27 +323,31 @@ hipError_t corr_forward_rows_f32(const void* in1, const void* in2, void* out, in
   const float inv = (mnt == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);
-#define PWC_ROWS(RR, M1, M2)                                                                  \
-  if (R == RR && per1 <= M1 && per2 <= M2) {                                                  \
+#define PWC_ROWS(TT, RR, M1, M2)                                                              \
+  if (sizeof(TT) == (h16 ? 2u : 4u) && R == RR && per1 <= M1 && per2 <= M2) {                 \
     static bool attr = false;                                                                 \
     if (!attr) {                                                                              \
       hipError_t e = hipFuncSetAttribute(                                                     \
-          reinterpret_cast<const void*>(&corr_fwd_rows<RR, NT, M1, M2>),                      \
+          reinterpret_cast<const void*>(&corr_fwd_rows<TT, RR, NT, M1, M2>),                  \
           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
       if (e != hipSuccess) return e;                                                          \
       attr = true;                                                                            \
     }                                                                                         \
-    hipExtLaunchKernelGGL((corr_fwd_rows<RR, NT, M1, M2>), dim3((unsigned)g.units), dim3(NT), \
-                          lds, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,     \
-                          (float*)out, C, H, W, divisor, inv, g, current_epi());              \
+    hipExtLaunchKernelGGL((corr_fwd_rows<TT, RR, NT, M1, M2>), dim3((unsigned)g.units),       \
+                          dim3(NT), lds, stream, ev0, ev1, 0, (const TT*)in1, (const TT*)in2, \
+                          (TT*)out, C, H, W, divisor, inv, g, current_epi());                 \
     return hipGetLastError();                                                                 \
   }
-  PWC_ROWS(3, 2, 7)   // l4 at CK 16: 1.75 / 6.4 loads per thread per chunk
-  PWC_ROWS(3, 1, 4)   // CK 8
-  PWC_ROWS(2, 2, 6)
-  PWC_ROWS(2, 1, 3)
-  PWC_ROWS(1, 1, 5)
-  PWC_ROWS(4, 2, 8)
+  PWC_ROWS(float, 3, 2, 7)   // l4 at CK 16: 1.75 / 6.4 loads per thread per chunk
+  PWC_ROWS(float, 3, 1, 4)   // CK 8
+  PWC_ROWS(float, 2, 2, 6)
+  PWC_ROWS(float, 2, 1, 3)
+  PWC_ROWS(float, 1, 1, 5)
+  PWC_ROWS(float, 4, 2, 8)
+  PWC_ROWS(_Float16, 2, 1, 3)
+  PWC_ROWS(_Float16, 2, 2, 6)
+  PWC_ROWS(_Float16, 1, 1, 3)
+  PWC_ROWS(_Float16, 1, 2, 5)
 #undef PWC_ROWS
   return hipErrorNotSupported;
 }
