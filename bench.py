@@ -611,9 +611,20 @@ def main(argv=None):
     C4, h4, w4 = shapes[-1]
     pairs = B * args.steps * world
     value = pairs / elapsed
+    shape_cfg = (B, args.height, args.width, args.dtype)
+    if shape_cfg == (8, 384, 448, "fp32"):
+        workload = ("BASELINE config 2 (config 3 at N>1): B=8 pairs/GPU, 384x448 fp32, warp + "
+                    "Correlation(pad 9, k 1, md 9, s1 1, s2 2) at levels l0-l4")
+    elif shape_cfg == (16, 448, 1024, "fp16"):
+        workload = ("BASELINE config 4: B=16 pairs/GPU, 448x1024 (Sintel shape) fp16 storage, "
+                    "warp + Correlation(pad 9, k 1, md 9, s1 1, s2 2) at levels l0-l4")
+    else:
+        workload = (f"custom: B={B} pairs/GPU, {args.height}x{args.width} {args.dtype}, warp + "
+                    "Correlation(pad 9, k 1, md 9, s1 1, s2 2) at levels l0-l4")
     result = {
-        "metric": "image-pairs/sec (forward, 384x448): hot path = WarpingLayer + Correlation(d=4)"
-                  " at all 5 pyramid levels; lvl2 corr HBM GB/s vs peak",
+        "metric": f"image-pairs/sec (forward, {args.height}x{args.width}): hot path = "
+                  "WarpingLayer + Correlation(d=4) at all 5 pyramid levels; lvl2 corr HBM GB/s "
+                  "vs peak",
         "value": round(value, 2),
         "unit": "image-pairs/s",
         "n_gpus": world,
@@ -627,8 +638,7 @@ def main(argv=None):
         "data": "synthetic (randn features / N(0,2^2) flows of the pyramid shapes; no weights on "
                 "this path)",
         "config": {
-            "workload": "BASELINE config 2 (config 3 at N>1): B=8 pairs/GPU, 384x448, warp + "
-                        "Correlation(pad 9, k 1, md 9, s1 1, s2 2) at levels l0-l4",
+            "workload": workload,
             "global_batch": B * world,
             "per_gpu_batch": B,
             "height": args.height,
