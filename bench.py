@@ -109,7 +109,10 @@ def parse_args(argv=None):
                     help="cpu = launcher rehearsal over gloo with a torch-CPU stand-in op")
     ap.add_argument("--fused-levels", default="0,1",
                     help="levels run as one fused warp->correlation launch (WarpCorrelation)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_l4corr_pmc.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02d_l4corr_pmc.json"),
+                    help="committed PMC summary used when the live passes cannot run")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live rocprofv3 PMC passes for roofline.traffic")
     return ap.parse_args(argv)
 
 
@@ -473,6 +476,55 @@ def load_pmc_traffic(path):
         return None, None
 
 
+def live_pmc_traffic(B, H, W, dtype, timeout=150):
+    """HBM bytes per launch of the l4 correlation measured NOW: two rocprofv3 PMC passes (one
+    counter each: FETCH_SIZE, WRITE_SIZE; MI355X_MICROARCH.md's HBM recipe) over
+    tools/kbench.py's l4 correlation at this run's shape, as child processes in their own
+    process group (killed as a group on timeout).  FETCH_SIZE counts half the bytes of
+    16-B-per-lane streaming reads on gfx950 -> x2; both in KB.  Returns (bytes, note) or
+    (None, reason)."""
+    import csv
+    import shutil
+    import signal
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    kb = {}
+    tmp = tempfile.mkdtemp(prefix="pwc_pmc_", dir="/tmp")
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = os.path.join(tmp, ctr)
+        cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "corr_fwd_stream", "-d", out, "-o",
+               "run", "--output-format", "csv", "--", sys.executable,
+               os.path.join(ROOT, "tools", "kbench.py"), "--levels", "4", "--ops", "corr",
+               "--iters", "20", "--batch", str(B), "--height", str(H), "--width", str(W),
+               "--dtype", dtype]
+        env = dict(os.environ, TMPDIR="/tmp")
+        p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+                             stderr=subprocess.DEVNULL, start_new_session=True)
+        try:
+            p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return None, f"rocprofv3 --pmc {ctr} timed out"
+        vals = []
+        for root, _, files in os.walk(out):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    for r in csv.DictReader(open(os.path.join(root, f))):
+                        if "corr_fwd_stream" in r["Kernel_Name"]:
+                            vals.append(float(r["Counter_Value"]))
+        if p.returncode != 0 or not vals:
+            return None, f"rocprofv3 --pmc {ctr} failed (rc {p.returncode})"
+        kb[ctr] = sum(vals) / len(vals)
+    shutil.rmtree(tmp, ignore_errors=True)
+    rd, wr = kb["FETCH_SIZE"] * 1024 * 2, kb["WRITE_SIZE"] * 1024
+    return int(rd + wr), (f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+                          f"tools/kbench.py --levels 4 in this run (reads {int(rd)} B with the "
+                          f"gfx950 x2 FETCH_SIZE correction, writes {int(wr)} B per launch)")
+
+
 # ---------------------------------------------------------------------------------------
 # main
 # ---------------------------------------------------------------------------------------
@@ -659,8 +711,14 @@ def main(argv=None):
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
         bytes_launch = corr_bytes_per_pair(C4, h4, w4, esz) * B
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-        traffic, tsrc = (load_pmc_traffic(args.pmc) if args.dtype == "fp32" and B == 8
-                         and (args.height, args.width) == (384, 448) else (None, None))
+        traffic, tsrc = None, None
+        if not args.no_pmc and rank == 0 and world == 1:
+            traffic, tsrc = live_pmc_traffic(B, args.height, args.width, args.dtype)
+        if traffic is None and args.dtype == "fp32" and (B, args.height, args.width) == (
+                8, 384, 448):
+            why = tsrc
+            traffic, tsrc = load_pmc_traffic(args.pmc)
+            tsrc = f"{tsrc} (committed; live PMC not taken: {why})"
         result["roofline"] = {
             "kernel": f"l4 correlation ({C4}x{h4}x{w4}, B={B}, {args.dtype}), start/stop events "
                       f"per timed step ({'hipExtLaunchKernel start/stop events'})",
