@@ -64,14 +64,24 @@ constexpr int next_8mod16(int v) { return v + ((8 - v % 16) + 16) % 16; }
 // parity per workgroup; 1: consecutive rows); R: output rows per workgroup; TWP: column tile
 // width in pixels (a lane owns an 8-pixel segment of it; wider images take several tiles);
 // CC: channels per ring stage; NS: ring depth in stages.
-template <typename T, int S2_, int R_, int TWP_, int CC_, int NS_>
+// P2 (fp16 storage only): LDS holds channel PAIRS -- pixel x of channels (c, c+1) as one
+// half2 dword, interleaved by the loader on the way in -- and every product pair is one
+// v_dot2_f32_f16 (two fp16 products, fp32 accumulation): per channel pair the fp32 kernel's LDS
+// traffic and instruction count, i.e. half of them per channel against v_fma_mix.
+template <typename T, int S2_, int R_, int TWP_, int CC_, int NS_, bool P2_ = false>
 struct Geo {
   using Elem = T;
   static constexpr int S2 = S2_, R = R_, TWP = TWP_, CC = CC_, NS = NS_;
-  static constexpr bool H16 = sizeof(T) == 2;
-  static constexpr int EPQ = 16 / (int)sizeof(T);        // elements per 16-B quad
+  static constexpr bool H16 = sizeof(T) == 2;            // fp16 storage (and output)
+  static constexpr bool P2 = P2_;
+  static_assert(!P2 || H16, "channel pairs are an fp16-storage layout");
+  static constexpr bool L16 = H16 && !P2;                // LDS holds single halves
+  static constexpr int CPU = P2 ? 2 : 1;                 // channels per ring unit
+  static constexpr int EPQ = L16 ? 8 : 4;                // LDS elements (pixels) per quad
+  static constexpr int OEPQ = 16 / (int)sizeof(T);       // output pixels per 16-B quad
   static constexpr int NPY = S2 == 2 ? 2 : 1;            // row parities split over workgroups
-  static constexpr int TWQ = TWP / EPQ;                  // tile quads per row
+  static constexpr int TWQ = TWP / EPQ;                  // tile quads per row (LDS)
+  static constexpr int OTWQ = TWP / OEPQ;                // tile quads per output row
   static constexpr int HQ = 8 / EPQ;                     // halo quads each side (8 pixels)
   static constexpr int SQ = 8 / EPQ;                     // quads per 8-pixel segment
   static constexpr int NSEG = TWP / 8;
@@ -80,10 +90,10 @@ struct Geo {
   static constexpr int BS = H16 ? 8 : (NSEG + NB - 1) / NB;
   // LDS row stride in quads: a ds_read_b128 lane group holds 8 segments of unit A and 8 of a
   // unit whose row differs by one, so their 16-B slots (mod 256 B) are disjoint iff S is odd
-  // (fp32: 2 quads per segment) or S = 8 mod 16 (fp16: 1 quad per segment)
-  static constexpr int S = H16 ? next_8mod16(TWQ + 2 * HQ) : ((TWQ + 2 * HQ) | 1);
-  static constexpr int NWQ = H16 ? 3 : (S2 == 2 ? 6 : 4);  // window quads read per channel
-  static constexpr int NFQ = H16 ? 1 : 2;                // f1 quads read per channel
+  // (fp32 / pairs: 2 quads per segment) or S = 8 mod 16 (halves: 1 quad per segment)
+  static constexpr int S = L16 ? next_8mod16(TWQ + 2 * HQ) : ((TWQ + 2 * HQ) | 1);
+  static constexpr int NWQ = L16 ? 3 : (S2 == 2 ? 6 : 4);  // window quads read per unit
+  static constexpr int NFQ = L16 ? 1 : 2;                // f1 quads read per unit
   static constexpr int F2R = R + 8;                      // f2 rows (tj = -4..4)
   static constexpr int F2Q = round64(F2R * S);           // quads of the f2 part of a channel
   static constexpr int F1Q = round64(R * S);
@@ -98,6 +108,10 @@ struct Geo {
   static constexpr int SLOT_B = CC * CH_B;               // one ring stage
   static constexpr int RING_B = NS * SLOT_B;
   static constexpr int PRQ = H16 ? 8 * NB : TWQ;         // park row quads (output staging)
+  // P2 loader: 8-pixel units (one 16-B global load per channel) of the staged rows
+  static constexpr int UPR = (TWP + 16) / 8;             // units per staged row
+  static constexpr int NU = (F2R + R) * UPR;             // units per channel pair
+  static constexpr int NIT = (NU + 63) / 64;             // loader iterations per pair
   static constexpr int OUT_B = 81 * R * PRQ * 16;
   static constexpr int LDS_BYTES = RING_B > OUT_B ? RING_B : OUT_B;
   static constexpr int NBASE = (RING_B + 32767) / 32768;  // 32 KiB address windows
@@ -106,7 +120,7 @@ struct Geo {
   static constexpr int WAITN = (NS - 3) * CC * IPC < 63 ? (NS - 3) * CC * IPC : 63;
   static_assert(S2 == 1 || S2 == 2, "displacement stride");
   static_assert(TWP % 8 == 0 && TWP % EPQ == 0 && BS <= 8, "8-pixel segments, <= 8 per block");
-  static_assert(H16 ? S % 16 == 8 : S % 2 == 1, "conflict-free row stride");
+  static_assert(L16 ? S % 16 == 8 : S % 2 == 1, "conflict-free row stride");
   static_assert(NS >= 4, "ring depth");
   static_assert(THREADS <= 1024 && LDS_BYTES <= 160 * 1024, "workgroup resources");
   static_assert(CH_B <= 32768, "a channel fits one 32 KiB window");
@@ -225,6 +239,39 @@ __device__ __forceinline__ void fma_ti_h(float (&acc)[9][8], const f32x4 (&w)[6]
   }
 }
 
+// Channel pairs: acc[ti][p] += f1[c][p] * w[c][p + S2 ti] + f1[c+1][p] * w[c+1][p + S2 ti]
+// as one v_dot2_f32_f16 per (ti, p); every LDS dword is one pixel's (c, c+1) half2.
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+template <int S2, int T0, int T1>
+__device__ __forceinline__ void fma_ti_p(float (&acc)[9][8], const f32x4 (&w)[6],
+                                         const f32x4 (&f)[2]) {
+#pragma unroll
+  for (int ti = T0; ti < T1; ++ti) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int j = p + S2 * ti;  // window element (quad j / 4), as fma_ti
+      // dword k of a quad as half2, built from the quad's 8 halves (bit-casting the k-th
+      // float / u32 element straight to half2 compiles to the quad's FIRST dword for every k
+      // with this toolchain -- checked in the ISA)
+      const f16x8 fh = __builtin_bit_cast(f16x8, f[p >> 2]);
+      const f16x8 wh = __builtin_bit_cast(f16x8, w[j >> 2]);
+      const h2_t a = {fh[2 * (p & 3)], fh[2 * (p & 3) + 1]};
+      const h2_t b = {wh[2 * (j & 3)], wh[2 * (j & 3) + 1]};
+      acc[ti][p] = __builtin_amdgcn_fdot2(a, b, acc[ti][p], false);
+    }
+  }
+}
+
+// fp32 or channel-pair products of displacements [T0, T1)
+template <class G, int T0, int T1>
+__device__ __forceinline__ void fma_unit(float (&acc)[9][8], const f32x4 (&w)[6],
+                                         const f32x4 (&f)[2]) {
+  if constexpr (G::P2)
+    fma_ti_p<G::S2, T0, T1>(acc, w, f);
+  else
+    fma_ti<G::S2, T0, T1>(acc, w, f);
+}
+
 // One DMA instruction of channel c's slot: `rel` = this lane's byte offset inside the channel
 // plane (or kOOB: the buffer unit returns zeros), `img` = the image's f1 or f2 base.
 __device__ __forceinline__ void dma1(const void* img, uint32_t cbytes, uint32_t img_bytes,
@@ -267,7 +314,7 @@ __device__ __forceinline__ void channel_body(uint32_t w_, uint32_t f_, float (&a
                                              const f32x4 (&wc)[6], const f32x4 (&fc)[2],
                                              f32x4 (&wn)[6], f32x4 (&fn)[2]) {
   constexpr bool RD = !(M & 1), FM = !(M & 2);
-  if constexpr (G::H16) {
+  if constexpr (G::L16) {
     constexpr int WEL = G::S2 == 2 ? 0 : 4;
     if constexpr (RD) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
     if constexpr (FM) fma_ti_h<G::S2, WEL, 0, 5>(acc, wc, fc);
@@ -276,25 +323,25 @@ __device__ __forceinline__ void channel_body(uint32_t w_, uint32_t f_, float (&a
     if constexpr (FM) fma_ti_h<G::S2, WEL, 5, 9>(acc, wc, fc);
   } else if constexpr (G::S2 == 2) {
     if constexpr (RD) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
-    if constexpr (FM) fma_ti<2, 0, 2>(acc, wc, fc);
+    if constexpr (FM) fma_unit<G, 0, 2>(acc, wc, fc);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RD) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
-    if constexpr (FM) fma_ti<2, 2, 4>(acc, wc, fc);
+    if constexpr (FM) fma_unit<G, 2, 4>(acc, wc, fc);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RD) read2<IMM + 64, IMM + 80>(w_, w_, wn[4], wn[5]);
-    if constexpr (FM) fma_ti<2, 4, 6>(acc, wc, fc);
+    if constexpr (FM) fma_unit<G, 4, 6>(acc, wc, fc);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RD) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
-    if constexpr (FM) fma_ti<2, 6, 9>(acc, wc, fc);
+    if constexpr (FM) fma_unit<G, 6, 9>(acc, wc, fc);
   } else {
     if constexpr (RD) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
-    if constexpr (FM) fma_ti<1, 0, 3>(acc, wc, fc);
+    if constexpr (FM) fma_unit<G, 0, 3>(acc, wc, fc);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RD) read2<IMM + 32, IMM + 48>(w_, w_, wn[2], wn[3]);
-    if constexpr (FM) fma_ti<1, 3, 6>(acc, wc, fc);
+    if constexpr (FM) fma_unit<G, 3, 6>(acc, wc, fc);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (RD) read2<IMM, IMM + 16>(f_, f_, fn[0], fn[1]);
-    if constexpr (FM) fma_ti<1, 6, 9>(acc, wc, fc);
+    if constexpr (FM) fma_unit<G, 6, 9>(acc, wc, fc);
   }
   if constexpr (!FM) asm volatile("" ::"v"(wc[0]), "v"(wc[2]), "v"(fc[0]));
 }
@@ -357,8 +404,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
   const int n = t / (ntx * nband * G::NPY);
   const int Y0 = band * G::R;         // first (parity) row of the band
   const int X0Q = tx * G::TWQ;        // first quad of the column tile
-  const int nst = C / G::CC;          // ring stages
-  const int WQ = W / G::EPQ;          // image quads per row
+  const int CU = C / G::CPU;          // ring units (channels, or channel pairs)
+  const int nst = CU / G::CC;         // ring stages
+  const int WQ = W / G::EPQ;          // image quads per row (LDS element units)
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -370,7 +418,105 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
   const uint32_t lds0 = lds_addr(lds);
   if (wave == 0) CENSUS(0);
 
-  if (wave == G::NWC) {
+  if (G::P2 && wave == G::NWC) {
+    // ---------------- loader wave, channel pairs: register staging ----------------
+    // 8-pixel units of channels c and c+1 (two 16-B loads; the buffer range check gives the
+    // zero border) interleaved into half2 quads (v_perm) and written with ds_write_b128.
+    // Stage s goes into its slot before B_{s+3-NS} ... i.e. up to stage k + NS - 3 is written
+    // before barrier B_k: the slot it reuses was last read before B_{k-1}.
+    constexpr uint32_t kOOB = 0x80000000u;
+    constexpr int NU2 = G::F2R * G::UPR, NU1 = G::R * G::UPR;
+    constexpr int NI2 = (NU2 + 63) / 64, NI1 = (NU1 + 63) / 64;
+    const int X0 = tx * G::TWP;
+    uint32_t rel2[NI2], rel1[NI1];
+    int dq2[NI2], dq1[NI1];
+#pragma unroll
+    for (int it = 0; it < NI2 + NI1; ++it) {
+      const bool f2 = it < NI2;
+      const int u = (f2 ? it : it - NI2) * 64 + lane;
+      const int rr = u / G::UPR, cu = u - rr * G::UPR;
+      const int prow = f2 ? Y0 - 4 + rr : Y0 + rr;
+      const int srow = G::S2 == 2 ? 2 * prow + py : prow;
+      const int px = X0 - 8 + 8 * cu;
+      const bool in = u < (f2 ? NU2 : NU1);
+      const bool ok = in && prow >= 0 && srow < H && px >= 0 && px < W;
+      const uint32_t rel = ok ? (uint32_t)(srow * W + px) * 2u : kOOB;
+      const int dq = in ? (f2 ? 0 : G::F2Q) + rr * G::S + 2 * cu : -1;
+      if (f2) rel2[it] = rel, dq2[it] = dq;
+      else rel1[it - NI2] = rel, dq1[it - NI2] = dq;
+    }
+    const __amdgpu_buffer_rsrc_t rs1 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)img1, (short)0, (int)img_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs2 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)img2, (short)0, (int)img_bytes, 0x00020000);
+    f32x4 a2[G::CC][NI2], b2[G::CC][NI2], a1[G::CC][NI1], b1[G::CC][NI1];
+    auto issue = [&](int gs) {
+#pragma unroll
+      for (int j = 0; j < G::CC; ++j) {
+        const int so = (int)((uint32_t)(2 * (gs * G::CC + j)) * plane_b);
+#pragma unroll
+        for (int it = 0; it < NI2; ++it) {
+          a2[j][it] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs2, (int)rel2[it], so, 0));
+          b2[j][it] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs2, (int)rel2[it],
+                                                           so + (int)plane_b, 0));
+        }
+#pragma unroll
+        for (int it = 0; it < NI1; ++it) {
+          a1[j][it] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs1, (int)rel1[it], so, 0));
+          b1[j][it] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs1, (int)rel1[it],
+                                                           so + (int)plane_b, 0));
+        }
+      }
+    };
+    // (c, c+1) halves of pixel k -> one dword: low half from channel c
+    auto put = [&](float* base, int dq, const f32x4& a, const f32x4& b) {
+      if (dq < 0) return;
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 av = __builtin_bit_cast(u32x4, a), bv = __builtin_bit_cast(u32x4, b);
+      const uint32_t ax = av.x, ay = av.y, az = av.z, aw = av.w;
+      const uint32_t bx = bv.x, by = bv.y, bz = bv.z, bw = bv.w;
+      const u32x4 q0 = {__builtin_amdgcn_perm(bx, ax, 0x05040100u),
+                        __builtin_amdgcn_perm(bx, ax, 0x07060302u),
+                        __builtin_amdgcn_perm(by, ay, 0x05040100u),
+                        __builtin_amdgcn_perm(by, ay, 0x07060302u)};
+      const u32x4 q1 = {__builtin_amdgcn_perm(bz, az, 0x05040100u),
+                        __builtin_amdgcn_perm(bz, az, 0x07060302u),
+                        __builtin_amdgcn_perm(bw, aw, 0x05040100u),
+                        __builtin_amdgcn_perm(bw, aw, 0x07060302u)};
+      *reinterpret_cast<u32x4*>(base + 4 * dq) = q0;
+      *reinterpret_cast<u32x4*>(base + 4 * dq + 4) = q1;
+    };
+    auto write = [&](int gs) {
+      float* slot = lds + (size_t)(gs % G::NS) * (G::SLOT_B / 4);
+#pragma unroll
+      for (int j = 0; j < G::CC; ++j) {
+        float* base = slot + j * (G::CH_B / 4);
+#pragma unroll
+        for (int it = 0; it < NI2; ++it) put(base, dq2[it], a2[j][it], b2[j][it]);
+#pragma unroll
+        for (int it = 0; it < NI1; ++it) put(base, dq1[it], a1[j][it], b1[j][it]);
+      }
+    };
+    if (abl & 2) {  // measurement: no staging (barriers only)
+      for (int k = 0; k <= nst; ++k) __builtin_amdgcn_s_barrier();
+    } else {
+      if (nst > 0) issue(0);
+      int nw = 0;  // next stage to write
+      for (int k = 0; k <= nst; ++k) {
+        const int upto = min(k + G::NS - 3, nst - 1);
+        while (nw <= upto) {
+          write(nw);
+          ++nw;
+          if (nw < nst) issue(nw);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B_k
+      }
+    }
+  } else if (wave == G::NWC) {
     // ---------------- loader wave ----------------
     constexpr uint32_t kOOB = 0x80000000u;
     uint32_t rel[G::IPC];
@@ -426,8 +572,8 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
     const int sg = seg < G::NSEG ? seg : 0;  // a duplicate address for idle lanes (broadcast)
     // window: from pixel x0 - 4 S2, i.e. padded pixel 8 seg + 8 - 4 S2 (fp32: quad 2 seg or
     // 2 seg + 1; fp16: quad seg, element 0 or 4); f1: padded pixel 8 seg + 8
-    const int wq = G::H16 ? sg : 2 * sg + (G::S2 == 2 ? 0 : 1);
-    const int fq = G::H16 ? sg + 1 : 2 * sg + 2;
+    const int wq = G::L16 ? sg : 2 * sg + (G::S2 == 2 ? 0 : 1);
+    const int fq = G::L16 ? sg + 1 : 2 * sg + 2;
     uint32_t wa[G::NBASE], fa[G::NBASE];
 #pragma unroll
     for (int k = 0; k < G::NBASE; ++k) {
@@ -447,7 +593,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
       acc[0][0] = (float)C;
     } else {
       __builtin_amdgcn_s_barrier();  // B_0: stage 0 landed
-      if constexpr (G::H16) {
+      if constexpr (G::L16) {
         read2<0, 16>(wa[0], wa[0], wA[0], wA[1]);
         read2<32, 0>(wa[0], fa[0], wA[2], fA[0]);
       } else {
@@ -457,11 +603,11 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
         read2<0, 16>(fa[0], fa[0], fA[0], fA[1]);
       }
       switch (abl >> 3) {
-        case 0: compute_loop<G, 0>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
-        case 1: compute_loop<G, 1>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
-        case 2: compute_loop<G, 2>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
-        case 5: compute_loop<G, 5>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
-        default: compute_loop<G, 6>(C, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        case 0: compute_loop<G, 0>(CU, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        case 1: compute_loop<G, 1>(CU, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        case 2: compute_loop<G, 2>(CU, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        case 5: compute_loop<G, 5>(CU, nst, wa, fa, acc, wA, fA, wB, fB); break;
+        default: compute_loop<G, 6>(CU, nst, wa, fa, acc, wA, fA, wB, fB); break;
       }
       lgk_wait<0>(wA, fA);  // the last (discarded) reads
     }
@@ -522,13 +668,15 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
   if (wave == 0) CENSUS(3);  // parked
   if (abl & 4) return;  // measurement: no stores
   T* oimg = out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * Ho * Wo);
-  constexpr int NQ = 81 * G::R * G::TWQ;
+  constexpr int OT = G::OTWQ;  // output quads per tile row
+  constexpr int NQ = 81 * G::R * OT;
   constexpr int PER = (NQ + G::THREADS - 1) / G::THREADS;
+  const int OWQ = W / G::OEPQ, OX0Q = tx * OT;
   st_f32x4 v[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {  // all LDS reads first, then all stores
     const int q = threadIdx.x + i * G::THREADS;
-    const int row = q / G::TWQ, xq = q - row * G::TWQ;
+    const int row = q / OT, xq = q - row * OT;
     int pq;
     if constexpr (G::H16) {
       pq = row * G::PRQ + (xq ^ (4 * ((xq / G::BS) & 1)));
@@ -541,12 +689,12 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int q = threadIdx.x + i * G::THREADS;
-    const int oc = q / (G::R * G::TWQ);
-    const int rem = q - oc * (G::R * G::TWQ);
-    const int r = rem / G::TWQ, xq = X0Q + rem - r * G::TWQ;
+    const int oc = q / (G::R * OT);
+    const int rem = q - oc * (G::R * OT);
+    const int r = rem / OT, xq = OX0Q + rem - r * OT;
     const int y = G::S2 == 2 ? 2 * (Y0 + r) + py : Y0 + r;
-    if (q < NQ && y < Ho && xq < WQ)
-      st_out4(reinterpret_cast<float*>(oimg + ((size_t)oc * Ho + y) * Wo + G::EPQ * xq), v[i]);
+    if (q < NQ && y < Ho && xq < OWQ)
+      st_out4(reinterpret_cast<float*>(oimg + ((size_t)oc * Ho + y) * Wo + G::OEPQ * xq), v[i]);
   }
   if (wave == 0) CENSUS(4);  // stores issued
 }
@@ -560,7 +708,7 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   const int ntx = (W + G::TWP - 1) / G::TWP;
   const long long nblk = (long long)B * G::NPY * nband * ntx;
   if (nblk <= 0) return hipSuccess;
-  if (C <= 0 || C % (G::NS * G::CC)) return hipErrorNotSupported;  // whole unrolled rounds
+  if (C <= 0 || C % (G::NS * G::CC * G::CPU)) return hipErrorNotSupported;  // whole rounds
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
@@ -590,6 +738,12 @@ static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C
   // 17.2 us against 2 x 8; Corr4, Sintel fp32/fp16 l3/l4; profiles/r02d_stream_ring_sweep.txt),
   // where one launch's store tail overlaps the next one's loop; inside the bench step, where
   // it cannot, all three rings measure the same 19.1-19.4 us (profiles/r02d_bench_ring_ab.txt)
+  // fp16: channel pairs through v_dot2_f32_f16 (stream_p2=0: single halves, v_fma_mix)
+  if constexpr (sizeof(T) == 2) {
+    if (debug_knob("stream_p2", 1) && C % 16 == 0)
+      return launch<Geo<T, S2, 3, TWP, 2, 4, true>>(in1, in2, out, B, C, H, W, layout, divisor,
+                                                    stream);
+  }
   switch (debug_knob("stream_cfg", 0)) {  // measurement variants (CC, NS)
     case 2: return launch<Geo<T, S2, 3, TWP, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
     case 8: return launch<Geo<T, S2, 3, TWP, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);

@@ -486,7 +486,11 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
   const bool scatter = debug_knob("warp_bwd", 1) == 0;  // 0: ATen-shaped atomic scatter
   if (!scatter) {
     // grad_x tile shape (knob warp_tiles for measurement)
-    const int tv = debug_knob("warp_tiles", 0);
+    // wide rows (l4: 96 x 112 at 384 x 448) take 16-channel tile groups and two channel groups
+    // in warp_bwd_flow: 55.3 -> 42.8 us at l4; narrower levels measured best at the defaults
+    // (profiles/r02d_bwd_knobs.txt)
+    const bool wide = W >= 96;
+    const int tv = debug_knob("warp_tiles", wide ? 2 : 0);
     int th = 8, tw = 32;
     if (C > 0) {
       hipError_t e = hipSuccess;
@@ -512,6 +516,7 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
     // channel groups for grids with few pixels (the coarse levels): ~64K threads or 16 groups
     int ng = 1;
     while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
+    if (wide && ng == 1 && C >= 32) ng = 2;
     if (const int k = debug_knob("warp_bwd_ng", 0)) ng = k;
     const int cpg = (C + ng - 1) / ng;
     const unsigned blocks = (unsigned)((npix * ng + 255) / 256);

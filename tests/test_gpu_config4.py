@@ -91,3 +91,26 @@ def test_stride1_full_size_l4_b8(sr_cfg):
         out, ref = cost_volume_forward(ta, tb, 4), O.cvl_forward(a, b, 4)
     torch.cuda.synchronize()
     np.testing.assert_allclose(_np(out), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape,md,s2", [((8, 32, 112, 256), 9, 2), ((16, 64, 56, 128), 9, 2),
+                                         ((8, 32, 112, 256), 4, 1)],
+                         ids=["l4_corr9", "l3_corr9", "l4_corr4"])
+def test_sintel_stream_fp16_channel_pairs(shape, md, s2):
+    """Config-4 batch sizes that reach the stream kernel: its fp16 channel-pair form (loader
+    interleaves channels c, c+1 into half2 dwords; v_dot2_f32_f16) against the oracle, and
+    against the single-half form (PWC_DEBUG stream_p2=0, v_fma_mix) -- both fp32 sums."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_forward
+    rng = np.random.default_rng(60 + shape[2] + md)
+    a, b = _h(rng, *shape), _h(rng, *shape)
+    out = corr_forward(a, b, md, 1, md, 1, s2)
+    _lib.set_debug("stream_p2=0")
+    try:
+        single = corr_forward(a, b, md, 1, md, 1, s2)
+    finally:
+        _lib.set_debug("")
+    torch.cuda.synchronize()
+    ref = O.corr_forward(_np(a), _np(b), md, 1, md, 1, s2)
+    _close_rel(_np(out), ref, 2e-3)
+    _close_rel(_np(single), ref, 2e-3)
