@@ -68,11 +68,11 @@ __device__ __forceinline__ f32x4 ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
 // GRAD 1: feat = f2, result g1.  GRAD 2: feat = f1, result g2.  CT channels per item and
 // chunk, ML staging loads per thread and chunk.
 template <int GRAD, bool VEC, int CT, int ML, int NT>
-__global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__ feat,
-                                                       const float* __restrict__ gout,
-                                                       float* __restrict__ gin, int C, int H,
-                                                       int W, float divisor, float inv_divisor,
-                                                       Geo g) {
+__device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ feat,
+                                                   const float* __restrict__ gout,
+                                                   float* __restrict__ gin, int C, int H,
+                                                   int W, float divisor, float inv_divisor,
+                                                   const Geo& g) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* stg = lds;
   f32x4* part = reinterpret_cast<f32x4*>(lds + g.stf);
@@ -260,6 +260,23 @@ __global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__
   }
 }
 
+// Both gradients in ONE launch: grid.z = 0 computes g1 from f2, grid.z = 1 g2 from f1 (the
+// two are independent; at the coarse levels each alone fills a fraction of the chip, so one
+// launch runs them side by side and saves a launch gap).
+template <bool VEC, int CT, int ML, int NT>
+__global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__ f1,
+                                                       const float* __restrict__ f2,
+                                                       const float* __restrict__ gout,
+                                                       float* __restrict__ g1,
+                                                       float* __restrict__ g2, int C, int H,
+                                                       int W, float divisor, float inv_divisor,
+                                                       Geo g) {
+  if (blockIdx.z == 0)
+    corr_bwd_rows_body<1, VEC, CT, ML, NT>(f2, gout, g1, C, H, W, divisor, inv_divisor, g);
+  else
+    corr_bwd_rows_body<2, VEC, CT, ML, NT>(f1, gout, g2, C, H, W, divisor, inv_divisor, g);
+}
+
 }  // namespace bwdrows
 
 // PWC_BWD_ROWS=0 disables the kernel; PWC_BWD_CFG="R,CT" forces a band height and channels per
@@ -332,22 +349,14 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
     static bool attr = false;                                                                  \
     if (!attr) {                                                                               \
       hipError_t e = hipFuncSetAttribute(                                                      \
-          reinterpret_cast<const void*>(&corr_bwd_rows<1, V, CTT, M, NT>),                     \
+          reinterpret_cast<const void*>(&corr_bwd_rows<V, CTT, M, NT>),                        \
           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                             \
-      if (e == hipSuccess)                                                                     \
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_bwd_rows<2, V, CTT, M, NT>), \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
       if (e != hipSuccess) return e;                                                           \
       attr = true;                                                                             \
     }                                                                                          \
-    hipLaunchKernelGGL((corr_bwd_rows<1, V, CTT, M, NT>), dim3(units, nsl), dim3(NT), lds, stream, \
-                       (const float*)in2, (const float*)gout, (float*)g1, C, H, W, divisor,    \
-                       inv, g);                                                                \
-    hipError_t e = hipGetLastError();                                                          \
-    if (e != hipSuccess) return e;                                                             \
-    hipLaunchKernelGGL((corr_bwd_rows<2, V, CTT, M, NT>), dim3(units, nsl), dim3(NT), lds, stream, \
-                       (const float*)in1, (const float*)gout, (float*)g2, C, H, W, divisor,    \
-                       inv, g);                                                                \
+    hipLaunchKernelGGL((corr_bwd_rows<V, CTT, M, NT>), dim3(units, nsl, 2), dim3(NT), lds,     \
+                       stream, (const float*)in1, (const float*)in2, (const float*)gout,       \
+                       (float*)g1, (float*)g2, C, H, W, divisor, inv, g);                      \
     return hipGetLastError();                                                                  \
   }
   PWC_BWD(true, 8, 2)
