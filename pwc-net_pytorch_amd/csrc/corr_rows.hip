@@ -278,18 +278,20 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
   if (W % epq != 0 || W < 8 || B == 0) return hipErrorNotSupported;
   if ((size_t)B * C * H * W >= (1ull << 30) || (size_t)B * 81 * H * W >= (1ull << 31))
     return hipErrorNotSupported;
-  // measured (tools/gpu_rows.sh, B=8 384x448): l2 (12 parity rows) stays on corr_pt.hip,
-  // l3 (24) R 2 -> 14.4 us against 16.1, l4 (48) R 3 -> 18.5 against 19.4 (kbench)
+  // measured (B=8 384x448, profiles/r02d_rows_sweep.txt): l2 (12 parity rows) R 1 / CK 48
+  // 9.7 us against corr_pt.hip's 11.7, l3 (24) R 2 / CK 32 13.1 against 14.4 (CK 16); fp16
+  // Sintel (B=16) l0 15.1 -> 12.9, l1 11.4 -> 10.1, l2 20.6 -> 19.9 against CK 16; the
+  // l4-sized grids belong to corr_stream.hip
   const int hp0 = (H + 1) / 2;
-  int R = hp0 <= 24 ? 2 : 3, CK = 16;
+  int R = hp0 <= 12 ? 1 : hp0 <= 24 ? 2 : 3, CK = hp0 <= 12 ? 48 : 32;
   if (debug_knob("rows_r", 0) > 0) {
     R = debug_knob("rows_r", R);
     CK = debug_knob("rows_ck", CK);
   } else if (h16) {
     R = hp0 <= 12 ? 1 : R;  // fp16 has no parity-tile / band kernel for the small levels
     if (hp0 > 24 && mode != 2) return hipErrorNotSupported;
-  } else if (hp0 <= 12 || (hp0 > 24 && mode != 2)) {
-    return hipErrorNotSupported;
+  } else if (hp0 <= 6 || (hp0 > 24 && mode != 2)) {
+    return hipErrorNotSupported;  // l0/l1-sized: the band kernel; l4-sized: the stream kernel
   }
   Geo g;
   g.Wq4 = ((W / 2) + 3) & ~3;
@@ -305,12 +307,16 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
   g.nb = (hp + R - 1) / R;
   g.units = B * 2 * g.nb;
   g.ck = CK < C ? CK : C;
-  g.f1f = g.ck * R * 2 * g.Wq4;
-  g.f2f = g.ck * (R + 8) * 2 * g.Wf;
-  const size_t stage = (size_t)(g.f1f + g.f2f) * 4;
-  const size_t red = (size_t)g.G * g.I * D * 16;
-  const size_t lds = stage > red ? stage : red;
-  if (lds > 160 * 1024) return hipErrorNotSupported;
+  size_t lds = 0;
+  for (;; g.ck = (g.ck + 1) / 2) {  // the largest chunk of channels that fits the LDS
+    g.f1f = g.ck * R * 2 * g.Wq4;
+    g.f2f = g.ck * (R + 8) * 2 * g.Wf;
+    const size_t stage = (size_t)(g.f1f + g.f2f) * 4;
+    const size_t red = (size_t)g.G * g.I * D * 16;
+    lds = stage > red ? stage : red;
+    if (lds <= 160 * 1024) break;
+    if (g.ck <= 4) return hipErrorNotSupported;
+  }
   const int per1 = (g.ck * R * g.Q + NT - 1) / NT;  // 16-B loads per thread per chunk
   const int per2 = (g.ck * (R + 8) * g.Q + NT - 1) / NT;
   g.inv_Q = 1.f / (float)g.Q;
@@ -344,6 +350,8 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
   PWC_ROWS(float, 2, 1, 3)
   PWC_ROWS(float, 1, 1, 5)
   PWC_ROWS(float, 4, 2, 8)
+  PWC_ROWS(float, 2, 2, 8)
+  PWC_ROWS(float, 1, 2, 8)
   PWC_ROWS(_Float16, 2, 1, 3)
   PWC_ROWS(_Float16, 2, 2, 6)
   PWC_ROWS(_Float16, 1, 1, 3)
