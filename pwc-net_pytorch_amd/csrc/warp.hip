@@ -232,10 +232,14 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
 // grad_x as a gather: a workgroup owns a TH x TW tile of grad_x (one pixel per thread) for
 // CC channels.  Every output pixel within M of the tile (its candidate window) recomputes its
 // sample (the forward's chain) and keeps the corners that fall in the tile; a counting sort in
-// LDS turns these into one list of (source pixel, bilinear weight) per tile pixel, sorted by
-// source pixel (deterministic).  Per channel a thread then sums gO * weight over its list in
-// registers and writes its grad_x element with a plain coalesced store: every element is
-// written once (no memset, no atomics, fixed summation order).  A corner whose pixel lies
+// LDS turns these into one list of (source pixel, bilinear weight) per tile pixel.  MODE 4:
+// each wave counts into its own row of slot counters, so a list holds wave 0's entries, then
+// wave 1's, ... each wave's in (candidate round, corner, lane) order -- a fixed order with no
+// sort (an LDS atomic orders one instruction's lanes by lane).  MODE 0: one shared counter row
+// (arrival order) and an insertion sort by source pixel.  Per channel a thread then sums
+// gO * weight over its list in registers (MODE 2: buffer loads at scalar channel offsets, two
+// entries in flight) and writes its grad_x element with a plain coalesced store: every
+// element is written once (no memset, no atomics, fixed summation order).  A corner whose pixel lies
 // outside the corner tile's candidate window (flow beyond ~M pixels) is left to
 // warp_bwd_flow, which adds it with a global atomic after this kernel (ATen's
 // grid_sampler_2d_backward adds every corner that way).
@@ -247,7 +251,7 @@ __device__ __forceinline__ bool bwd_in_window(int py, int px, int cy, int cx, in
          px < tx0 + tw + kBwdM;
 }
 
-template <int TW, int CC>
+template <int TW, int CC, int MODE = 0>
 __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict__ flow,
                                                          const float* __restrict__ gout,
                                                          float* __restrict__ gx, int C, int H,
@@ -256,7 +260,8 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
   constexpr int TH = 256 / TW, M = kBwdM;
   constexpr int WW = TW + 2 * M, NCAND = (TH + 2 * M) * WW, K = (NCAND + 255) / 256;
   constexpr int MAXL = 4 * NCAND;
-  __shared__ int cnt[256];
+  constexpr bool WAVEC = (MODE & 4) != 0;  // per-wave slot counters: list order fixed, no sort
+  __shared__ int cnt[WAVEC ? 4 * 256 : 256];
   __shared__ int wsum[4];
   __shared__ unsigned lpix[MAXL];
   __shared__ float lw[MAXL];
@@ -265,7 +270,9 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
   const int n = blockIdx.y, c0 = blockIdx.z * CC;
   const int y0 = ty * TH, x0 = tx * TW;
   const unsigned plane = (unsigned)(H * W);
+  const int cw = WAVEC ? (t >> 6) * 256 : 0;  // this wave's counter row
   cnt[t] = 0;
+  if (WAVEC) cnt[256 + t] = cnt[512 + t] = cnt[768 + t] = 0;
   int slot[K][4];
   float wt[K][4];
   unsigned pix[K];
@@ -298,9 +305,12 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
 #pragma unroll
   for (int j = 0; j < K; ++j)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) pos[j][k] = slot[j][k] >= 0 ? atomicAdd(&cnt[slot[j][k]], 1) : 0;
+    for (int k = 0; k < 4; ++k)
+      pos[j][k] = slot[j][k] >= 0 ? atomicAdd(&cnt[cw + slot[j][k]], 1) : 0;
   __syncthreads();
-  const int len = cnt[t];
+  int wc[4] = {cnt[t], 0, 0, 0};
+  if (WAVEC) wc[1] = cnt[256 + t], wc[2] = cnt[512 + t], wc[3] = cnt[768 + t];
+  const int len = wc[0] + wc[1] + wc[2] + wc[3];
   int incl = len;  // inclusive scan: within the wave, then over the 4 waves
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -312,19 +322,24 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
   for (int w = 0; w < (t >> 6); ++w) incl += wsum[w];
   const int start = incl - len;
   cnt[t] = start;
+  if (WAVEC) {
+    cnt[256 + t] = start + wc[0];
+    cnt[512 + t] = start + wc[0] + wc[1];
+    cnt[768 + t] = start + wc[0] + wc[1] + wc[2];
+  }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < K; ++j)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (slot[j][k] >= 0) {
-        const int e = cnt[slot[j][k]] + pos[j][k];
+        const int e = cnt[cw + slot[j][k]] + pos[j][k];
         lpix[e] = pix[j];
         lw[e] = wt[j][k];
       }
   __syncthreads();
   // my list, sorted by source pixel (insertion sort: a few entries)
-  for (int i = start + 1; i < start + len; ++i) {
+  for (int i = start + 1; i < (WAVEC ? 0 : start + len); ++i) {
     const unsigned pk = lpix[i];
     const float wk = lw[i];
     int j = i - 1;
@@ -343,7 +358,29 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
   float acc[CC];
 #pragma unroll
   for (int i = 0; i < CC; ++i) acc[i] = 0.f;
-  for (int e = start; e < start + len; ++e) {
+  int e0 = start;
+  if (MODE & 2) {
+    // channel planes at scalar offsets of one buffer resource, two list entries in flight
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)go, (short)0, (int)((unsigned)cn * plane * 4u), 0x00020000);
+    for (; e0 + 1 < start + len; e0 += 2) {
+      const unsigned p0 = lpix[e0], p1 = lpix[e0 + 1];
+      const float w0 = lw[e0], w1 = lw[e0 + 1];
+      float g0[CC], g1[CC];
+#pragma unroll
+      for (int i = 0; i < CC; ++i) {
+        g0[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rs, (int)(p0 * 4u), (int)(i * plane * 4u), 0));
+        g1[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rs, (int)(p1 * 4u), (int)(i * plane * 4u), 0));
+      }
+#pragma unroll
+      for (int i = 0; i < CC; ++i) acc[i] += g0[i] * w0;
+#pragma unroll
+      for (int i = 0; i < CC; ++i) acc[i] += g1[i] * w1;
+    }
+  }
+  for (int e = e0; e < start + len; ++e) {
     const unsigned p = lpix[e];
     const float w = lw[e];
     float g[CC];
@@ -362,7 +399,7 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
 // pixels x NG channel groups (lanes of a wave = consecutive pixels of one group); group g
 // takes channels [g*cpg, (g+1)*cpg) and the NG partial sums meet in LDS in group order
 // (deterministic; NG = 1 is ATen's channel loop order).
-template <int CB, int NG>
+template <int CB, int NG, bool PAIRS = false>
 __global__ __launch_bounds__(256) void warp_bwd_flow(const float* __restrict__ x,
                                                      const float* __restrict__ flow,
                                                      const float* __restrict__ gout,
@@ -388,6 +425,7 @@ __global__ __launch_bounds__(256) void warp_bwd_flow(const float* __restrict__ x
   const float iy = src_coord(v, py, H, halfy);
   const Bilinear b = bilinear(ix, iy, H, W);
   const Corners k = corners(b, H, W);
+  const Pairs kp = pairs(b, H, W);
   const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;
   const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
   // corners outside their tile's candidate window (rare: |flow| beyond ~kBwdM)
@@ -400,15 +438,29 @@ __global__ __launch_bounds__(256) void warp_bwd_flow(const float* __restrict__ x
   const int cs = grp * cpg, ce = live ? min(C, cs + cpg) : cs;
   for (int c0 = cs; c0 < ce; c0 += CB) {
     float r[CB][4], go[CB];
+    if (PAIRS && W >= 2) {  // both corners of a sample row from one 8-byte load
+      WarpGroup<float, CB> wg;
+      warp_load(wg, x, n, C, plane, c0, W, kp, k);
 #pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int c = min(c0 + i, ce - 1);
-      const float* p = x + ((unsigned)(n * C + c)) * plane;
-      r[i][0] = masked(p[k.i00], k.m00);
-      r[i][1] = masked(p[k.i01], k.m01);
-      r[i][2] = masked(p[k.i10], k.m10);
-      r[i][3] = masked(p[k.i11], k.m11);
-      go[i] = (c0 + i < ce) ? gout[((unsigned)(n * C + c)) * plane + pix] : 0.f;
+      for (int i = 0; i < CB; ++i) {
+        r[i][0] = masked(wg.r[i][0], k.m00);
+        r[i][1] = masked(wg.r[i][1], k.m01);
+        r[i][2] = masked(wg.r[i][2], k.m10);
+        r[i][3] = masked(wg.r[i][3], k.m11);
+        const int c = min(c0 + i, ce - 1);
+        go[i] = (c0 + i < ce) ? gout[((unsigned)(n * C + c)) * plane + pix] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CB; ++i) {
+        const int c = min(c0 + i, ce - 1);
+        const float* p = x + ((unsigned)(n * C + c)) * plane;
+        r[i][0] = masked(p[k.i00], k.m00);
+        r[i][1] = masked(p[k.i01], k.m01);
+        r[i][2] = masked(p[k.i10], k.m10);
+        r[i][3] = masked(p[k.i11], k.m11);
+        go[i] = (c0 + i < ce) ? gout[((unsigned)(n * C + c)) * plane + pix] : 0.f;
+      }
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
@@ -494,23 +546,32 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
     int th = 8, tw = 32;
     if (C > 0) {
       hipError_t e = hipSuccess;
-#define PWC_TILES(V, TW, CC)                                                                   \
-  if (tv == V) {                                                                               \
+      // list build: 6 = per-wave slot counters + buffer-load gathers two entries deep (l4 42.8
+      // -> 36.0 us with the flow kernel's paired loads, l3 28.2 -> 22.8, l2 21.2 -> 17.4:
+      // profiles/r02e_warp_bwd_modes.txt); 0 = the atomic counting sort + insertion sort
+      const int gm = debug_knob("wbg_mode", 6);
+#define PWC_TILES_M(V, TW, CC, M)                                                              \
+  if (tv == V && gm == M) {                                                                    \
     th = 256 / TW;                                                                             \
     tw = TW;                                                                                   \
     const int ntx = (W + TW - 1) / TW, nty = (H + th - 1) / th;                                \
-    hipLaunchKernelGGL((warp_bwd_gx_lists<TW, CC>),                                            \
+    hipLaunchKernelGGL((warp_bwd_gx_lists<TW, CC, M>),                                         \
                        dim3((unsigned)(ntx * nty), (unsigned)B, (unsigned)((C + CC - 1) / CC)), \
                        dim3(256), 0, stream, (const float*)flow, (const float*)gout,           \
                        (float*)gx, C, H, W, halfx, halfy, ntx);                                \
     e = hipGetLastError();                                                                     \
   }
+#define PWC_TILES(V, TW, CC) PWC_TILES_M(V, TW, CC, 0) PWC_TILES_M(V, TW, CC, 6)
       PWC_TILES(0, 32, 8)
       PWC_TILES(1, 32, 4)
       PWC_TILES(2, 32, 16)
       PWC_TILES(3, 16, 8)
       PWC_TILES(4, 64, 8)
+      PWC_TILES(5, 32, 32)
+      PWC_TILES(6, 16, 16)
+      PWC_TILES(7, 64, 16)
 #undef PWC_TILES
+#undef PWC_TILES_M
       if (e != hipSuccess) return e;
     }
     // channel groups for grids with few pixels (the coarse levels): ~64K threads or 16 groups
@@ -520,19 +581,22 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
     if (const int k = debug_knob("warp_bwd_ng", 0)) ng = k;
     const int cpg = (C + ng - 1) / ng;
     const unsigned blocks = (unsigned)((npix * ng + 255) / 256);
-#define PWC_FLOW(NGV)                                                                          \
-  if (ng == NGV) {                                                                             \
-    hipLaunchKernelGGL((warp_bwd_flow<8, NGV>), dim3(blocks), dim3(256), 0, stream,            \
+    const bool fpairs = debug_knob("wbf_pairs", 1) != 0;  // 8-byte corner-pair gathers
+#define PWC_FLOW_P(NGV, PR)                                                                    \
+  if (ng == NGV && fpairs == PR) {                                                             \
+    hipLaunchKernelGGL((warp_bwd_flow<8, NGV, PR>), dim3(blocks), dim3(256), 0, stream,        \
                        (const float*)x, (const float*)flow, (const float*)gout, (float*)gx,    \
                        (float*)gflow, B, C, H, W, halfx, halfy, cpg, th, tw);                  \
     return hipGetLastError();                                                                  \
   }
+#define PWC_FLOW(NGV) PWC_FLOW_P(NGV, false) PWC_FLOW_P(NGV, true)
     PWC_FLOW(1)
     PWC_FLOW(2)
     PWC_FLOW(4)
     PWC_FLOW(8)
     PWC_FLOW(16)
 #undef PWC_FLOW
+#undef PWC_FLOW_P
     return hipErrorNotSupported;
   }
   // PWC_WARP_BWD=0: the scatter of ATen's kernel (global atomics into a zeroed grad_x)

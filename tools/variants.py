@@ -67,12 +67,18 @@ def main():
         _lib.set_debug(knob)
         out = fn(sets[0])
         out = list(out) if isinstance(out, tuple) else [out]
-        diff = max(float(((a.float() - b.float()).abs() / (1 + b.float().abs())).max())
-                   for a, b in zip(out, ref))
+        diffs = [float(((a.float() - b.float()).abs() / (1 + b.float().abs())).max())
+                 for a, b in zip(out, ref)]
+        diff = max(diffs)
+        out = [o.clone() for o in out]
+        rep = [fn(sets[0]) for _ in range(3)]
+        same = all(torch.equal(a, b) for r in rep
+                   for a, b in zip(list(r) if isinstance(r, tuple) else [r], out))
         med, mn = timeit(fn, sets, args.iters)
         print(json.dumps(dict(op=args.op, level=args.level, dtype=args.dtype, knob=knob or "default",
                               us=round(med, 2), min_us=round(mn, 2),
-                              gbs=round(nbytes / (med * 1e-6) / 1e9, 1), max_rel_diff=diff)),
+                              gbs=round(nbytes / (med * 1e-6) / 1e9, 1), max_rel_diff=diff, diffs=diffs,
+                              repeatable=same)),
               flush=True)
     _lib.set_debug("")
 
