@@ -298,10 +298,10 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   g.Wq4 = (((W + 1) / 2) + 3) & ~3;
   g.Wf = g.Wq4 + 8;
   g.S = g.Wq4 / 4;
-  // the tallest band (least restaging of the R + 8 feature rows); channel slices fill the chip
-  // CT 8 measured 17.2 against 22.9 us (4) at l2, equal at l3/l4; 4 on the dword path (l0/l1:
-  // 17.2 / 18.5 against 20.1 / 21.8 us)
-  int R = 1, CT = vec ? 8 : 4;
+  // the tallest band (least restaging of the R + 8 feature rows); channel slices fill the chip.
+  // CT 8 (channels per item and chunk) except on the dword path at 192 channels (l0: 4 gives
+  // the chunks for 4 slices, 10.7 against 11.5 us); profiles/r02e_corr_bwd_slices.txt
+  int R = 1, CT = (vec || C < 192) ? 8 : 4;
   for (int r : {3, 2, 1}) {
     if (9 * r * 2 * g.S > NT) continue;
     R = r;
@@ -325,12 +325,14 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   }
   g.lw = vec ? W / 4 : W;
   g.nld = g.ck * (R + 8) * g.lw;
-  // channel slices (grid.y) up to about one workgroup per CU: the slices of a band are
-  // independent (every gradient element is one channel's) but each re-reads the band's gO
+  // channel slices (grid.y) up to one workgroup per CU over both gradients (grid.z): the
+  // slices of a band are independent (every gradient element is one channel's) but each
+  // re-reads the band's gO.  Measured (B = 8, 384 x 448): l1 16.0 -> 12.3 us (CT 8, 3
+  // slices), l2 17.0 -> 12.7 (2), l3 27.7 -> 23.2 (1), l0 / l4 unchanged (4 / 1)
   const long long bands = (long long)B * 2 * ((hp + R - 1) / R);
   const int nchunks = (C + g.ck - 1) / g.ck;
   int nsl = 1;
-  while (nsl < nchunks && bands * (nsl + 1) <= 320) ++nsl;  // measured: 1 at l4, 2 at l3
+  while (nsl < nchunks && bands * 2 * (nsl + 1) <= 256) ++nsl;
   if (const int k = debug_knob("bwd_slices", 0)) nsl = std::max(1, std::min(nchunks, k));
   g.cps = ((nchunks + nsl - 1) / nsl) * g.ck;
   nsl = (C + g.cps - 1) / g.cps;
