@@ -740,9 +740,19 @@ static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C
   // it cannot, all three rings measure the same 19.1-19.4 us (profiles/r02d_bench_ring_ab.txt)
   // fp16: channel pairs through v_dot2_f32_f16 (stream_p2=0: single halves, v_fma_mix)
   if constexpr (sizeof(T) == 2) {
-    if (debug_knob("stream_p2", 1) && C % 16 == 0)
+    if (debug_knob("stream_p2", 1) && C % 16 == 0) {
+      // 4-row bands when 3-row bands give few workgroups (about one round): config-4 Sintel
+      // l3 (B=16, 64 x 56 x 128) 41.6 -> 28.0 us; l4 (1216 workgroups) stays at 3 (63.3 against
+      // 66.4 us; 2 rows 75.4); profiles/r02e_stream_fp16_rows.txt
+      const int hp = S2 == 2 ? (H + 1) / 2 : H;
+      const long long nblk3 = (long long)B * (S2 == 2 ? 2 : 1) * ((hp + 2) / 3) *
+                              ((W + TWP - 1) / TWP);
+      if (debug_knob("stream_r", nblk3 <= 384 ? 4 : 3) == 4)
+        return launch<Geo<T, S2, 4, TWP, 2, 4, true>>(in1, in2, out, B, C, H, W, layout, divisor,
+                                                      stream);
       return launch<Geo<T, S2, 3, TWP, 2, 4, true>>(in1, in2, out, B, C, H, W, layout, divisor,
                                                     stream);
+    }
   }
   switch (debug_knob("stream_cfg", 0)) {  // measurement variants (CC, NS)
     case 2: return launch<Geo<T, S2, 3, TWP, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);

@@ -94,12 +94,15 @@ def test_stride1_full_size_l4_b8(sr_cfg):
 
 
 @pytest.mark.parametrize("shape,md,s2", [((8, 32, 112, 256), 9, 2), ((16, 64, 56, 128), 9, 2),
-                                         ((8, 32, 112, 256), 4, 1)],
-                         ids=["l4_corr9", "l3_corr9", "l4_corr4"])
+                                         ((8, 32, 112, 256), 4, 1), ((16, 32, 55, 128), 9, 2),
+                                         ((12, 16, 54, 128), 4, 1)],
+                         ids=["l4_corr9", "l3_corr9", "l4_corr4", "rows4_odd_h_tail",
+                              "rows4_corr4_tail"])
 def test_sintel_stream_fp16_channel_pairs(shape, md, s2):
     """Config-4 batch sizes that reach the stream kernel: its fp16 channel-pair form (loader
     interleaves channels c, c+1 into half2 dwords; v_dot2_f32_f16) against the oracle, and
-    against the single-half form (PWC_DEBUG stream_p2=0, v_fma_mix) -- both fp32 sums."""
+    against the single-half form (PWC_DEBUG stream_p2=0, v_fma_mix) -- both fp32 sums.  The
+    smaller grids take 4-row bands (l3; odd H and bands cut short at the image's last rows)."""
     from pwcnet_amd import _lib
     from pwcnet_amd.ops import corr_forward
     rng = np.random.default_rng(60 + shape[2] + md)
