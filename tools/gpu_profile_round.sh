@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round profile r02d -> gpurun_out/prof_r02d: default bench (CPU baselines, live PMC traffic),
+# Round profile TAG (default r02e) -> gpurun_out/prof_TAG: default bench (CPU baselines, live PMC traffic),
 # graph-all comparison, rocprofv3 kernel stats of the bench, committed-PMC summary of the l4
 # correlation, per-level kbench incl. backward, training step (+ kernel stats), config 4.
 set -o pipefail
-OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_r02d
+OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG:-r02e}
 mkdir -p $OUT
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
