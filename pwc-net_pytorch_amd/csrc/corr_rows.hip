@@ -17,6 +17,8 @@
 // window is 3 aligned quads).  Rows outside the image come back as zeros from the buffer range
 // check, so no LDS clear is needed per chunk.
 //
+// Optionally (TS = 2) the 9 displacement rows tj are split between two workgroups of a band
+// (each stages the R + 4 or R + 3 f2 rows its tj meet).
 // Compute: item = (tj, row, column parity, 4-pixel segment); per channel 1 f1 quad + 3 f2
 // quads feed 36 FMAs (0.44 LDS floats per FMA).  G = NT / items channel groups meet in LDS in a
 // fixed order (deterministic).  The result block is written row by row as 16-byte
@@ -44,13 +46,16 @@ struct Geo {
   int Wf;    // f2 row half slots: Wq4 + 8
   int S;     // 4-pixel segments per row half
   int Q;     // 16-byte quads per image row (W / 4)
-  int I;     // compute items: 9 * R * 2 * S
+  int TS;    // displacement-row groups: a workgroup takes DT = ceil(9 / TS) rows tj
+  int DT;
+  int NR2;   // staged f2 rows: R + DT - 1
+  int I;     // compute items: DT * R * 2 * S
   int G;     // channel groups
   int nb;    // bands per parity half
-  int units; // B * 2 * nb
+  int units; // B * 2 * nb * TS
   int ck;    // channels per chunk
   int f1f;   // floats of one chunk's f1 image: ck * R * 2 * Wq4
-  int f2f;   // floats of one chunk's f2 image: ck * (R + 8) * 2 * Wf
+  int f2f;   // floats of one chunk's f2 image: ck * NR2 * 2 * Wf
   float inv_Q, inv_NR2, inv_I, inv_S, inv_W4;
 };
 
@@ -75,9 +80,11 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
   constexpr int EPQ = 16 / (int)sizeof(T);  // pixels per 16-B quad
   constexpr int HPQ = EPQ / 2;              // parity slots per quad and column parity
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int NR2 = R + 8;
+  const int NR2 = g.NR2;
   const int t = threadIdx.x;
-  const int unit = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring bands share an L2
+  const int unit0 = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring bands share an L2
+  const int tg = unit0 % g.TS, unit = unit0 / g.TS;    // displacement-row group
+  const int tj0 = tg * g.DT;
   const int b = unit % g.nb, np = unit / g.nb;
   const int p = np & 1, n = np >> 1;
   const int hp = (H - p + 1) >> 1;
@@ -129,7 +136,7 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
     const int itm = t + j * NT;
     const int rest = qdiv(itm, g.inv_Q), qd = itm - rest * g.Q;
     const int c = qdiv(rest, g.inv_NR2), k = rest - c * NR2;
-    const int rr = r0 - 4 + k;
+    const int rr = r0 - 4 + tj0 + k;
     const bool ok = itm < tot2 && rr >= 0 && rr < hp;
     vo2[j] = ok ? ((uint32_t)c * plane + (uint32_t)(2 * rr + p) * W + EPQ * qd) *
                       (uint32_t)sizeof(T)
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
   int rest = qdiv(it, g.inv_S);
   const int q = rest & 1;
   rest >>= 1;
-  const int r = rest % R, tt = rest / R;
+  const int r = rest % R, tt = rest / R;  // tj = tj0 + tt
   const int a_off = (r * 2 + q) * g.Wq4 + 4 * s;
   const int b_off = g.f1f + ((r + tt) * 2 + q) * g.Wf + 4 * s;
   const int s1c = R * 2 * g.Wq4, s2c = NR2 * 2 * g.Wf;  // floats per channel
@@ -223,20 +230,20 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
 
   // ---- epilogue: lane = 4 consecutive x of one (tj, ti, row); fixed-order group sum ----
   const int W4 = W >> 2;
-  const int nout = D * D * R * W4;
+  const int nout = g.DT * D * R * W4;
   const int gstride = g.I * D * 4;
   for (int o = t; o < nout; o += NT) {
     const int m = o - qdiv(o, g.inv_W4) * W4;  // x = 4m .. 4m+3
     int rr2 = qdiv(o, g.inv_W4);
     const int rowi = rr2 % R;
     rr2 /= R;
-    const int ti = rr2 % D, tj = rr2 / D;
+    const int ti = rr2 % D, tt = rr2 / D, tj = tj0 + tt;
     const int row = r0 + rowi;
-    if (row >= hp) continue;
+    if (row >= hp || tj >= D) continue;
     // x = 4m + e: parity e & 1, parity slot i = 2m + (e >> 1) -> segment s = i >> 2, kk = i & 3
     const int i0 = 2 * m, sg = i0 >> 2, kk = i0 & 3;  // kk in {0, 2}
-    const int it0 = ((tj * R + rowi) * 2 + 0) * g.S + sg;
-    const int it1 = ((tj * R + rowi) * 2 + 1) * g.S + sg;
+    const int it0 = ((tt * R + rowi) * 2 + 0) * g.S + sg;
+    const int it1 = ((tt * R + rowi) * 2 + 1) * g.S + sg;
     const float* p0 = lds + (it0 * D + ti) * 4 + kk;
     const float* p1 = lds + (it1 * D + ti) * 4 + kk;
     f32x2 e0 = *reinterpret_cast<const f32x2*>(p0);
@@ -298,19 +305,35 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
   g.Wf = g.Wq4 + 8;
   g.S = g.Wq4 / 4;
   g.Q = W / epq;
-  g.I = D * R * 2 * g.S;
+  // 13..24 parity rows: 3-row bands split into two displacement-row groups (tj 0-4 / 5-8:
+  // 7 staged f2 rows instead of 11) when that fills the workgroup rounds better than 2-row
+  // bands -- config-2 l3: 256 workgroups instead of 192, 14.2 -> 13.1 us
+  // (profiles/r02e_rows_tj_groups.txt); Sintel fp16 l2 keeps 2-row bands (224 against 320)
+  g.TS = 1;
+  if (hp0 > 12 && hp0 <= 24 && debug_knob("rows_r", 0) == 0) {
+    const long long u2 = (long long)B * 2 * ((hp0 + 1) / 2);
+    const long long u3 = (long long)B * 2 * ((hp0 + 2) / 3) * 2;
+    auto fill = [](long long u) { return (double)u / (256.0 * (double)((u + 255) / 256)); };
+    if (fill(u3) > fill(u2)) R = 3, g.TS = 2;
+  }
+  g.TS = debug_knob("rows_ts", g.TS);
+  if (g.TS < 1 || g.TS > D) return hipErrorNotSupported;
+  g.DT = (D + g.TS - 1) / g.TS;
+  g.TS = (D + g.DT - 1) / g.DT;  // no empty groups
+  g.NR2 = R + g.DT - 1;
+  g.I = g.DT * R * 2 * g.S;
   constexpr int NT = 768;
   if (g.I > NT || R < 1) return hipErrorNotSupported;
   g.G = NT / g.I;
   if (g.G > C) g.G = C;
   const int hp = (H + 1) / 2;
   g.nb = (hp + R - 1) / R;
-  g.units = B * 2 * g.nb;
+  g.units = B * 2 * g.nb * g.TS;
   g.ck = CK < C ? CK : C;
   size_t lds = 0;
   for (;; g.ck = (g.ck + 1) / 2) {  // the largest chunk of channels that fits the LDS
     g.f1f = g.ck * R * 2 * g.Wq4;
-    g.f2f = g.ck * (R + 8) * 2 * g.Wf;
+    g.f2f = g.ck * g.NR2 * 2 * g.Wf;
     const size_t stage = (size_t)(g.f1f + g.f2f) * 4;
     const size_t red = (size_t)g.G * g.I * D * 16;
     lds = stage > red ? stage : red;
@@ -318,9 +341,9 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
     if (g.ck <= 4) return hipErrorNotSupported;
   }
   const int per1 = (g.ck * R * g.Q + NT - 1) / NT;  // 16-B loads per thread per chunk
-  const int per2 = (g.ck * (R + 8) * g.Q + NT - 1) / NT;
+  const int per2 = (g.ck * g.NR2 * g.Q + NT - 1) / NT;
   g.inv_Q = 1.f / (float)g.Q;
-  g.inv_NR2 = 1.f / (float)(R + 8);
+  g.inv_NR2 = 1.f / (float)g.NR2;
   g.inv_I = 1.f / (float)g.I;
   g.inv_S = 1.f / (float)g.S;
   g.inv_W4 = 1.f / (float)(W / 4);
