@@ -257,8 +257,9 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
       v4 *= inv_divisor;
     else
       v4 = f32x4{v4.x / divisor, v4.y / divisor, v4.z / divisor, v4.w / divisor};
-    v4 = f32x4{epi_act(v4.x, epi.slope), epi_act(v4.y, epi.slope), epi_act(v4.z, epi.slope),
-               epi_act(v4.w, epi.slope)};
+    if (epi.slope != 1.f)  // model.py:84's leaky_relu, fused only when asked for
+      v4 = f32x4{epi_act(v4.x, epi.slope), epi_act(v4.y, epi.slope), epi_act(v4.z, epi.slope),
+                 epi_act(v4.w, epi.slope)};
     const size_t ib = epi.ostride ? (size_t)n * epi.ostride : (size_t)n * (D * D) * H * W;
     T* dst = out + ib + ((size_t)(tj * D + ti) * H + (2 * row + p)) * W + 4 * m;
     if constexpr (H16)

@@ -31,6 +31,7 @@
 #include <hip/hip_ext.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "pwc_common.cuh"
 
@@ -637,29 +638,40 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
             acc[ti][k] = fmaf(fmaf(-q, divisor, acc[ti][k]), rinv, q);
           }
       }
+      // the fused leaky_relu (model.py:84) only when asked for: a uniform branch, so the
+      // plain volume parks its 72 values with no per-value compare / select
+      auto park = [&](auto act_c) {
+        constexpr bool ACT = decltype(act_c)::value;
 #pragma unroll
-      for (int ti = 0; ti < 9; ++ti) {
-        const int oc = out_channel(layout, tj - 4, ti - 4, 4, 9, G::S2);
-        f32x4* prow = reinterpret_cast<f32x4*>(lds) + (oc * G::R + r) * G::PRQ;
-        if constexpr (G::H16) {
-          // one quad per lane; odd segment blocks XOR 4 so the two blocks sharing a
-          // ds_write_b128 lane group (8 consecutive lanes) hit disjoint 16-B slots
-          f16x8 v;
+        for (int ti = 0; ti < 9; ++ti) {
+          const int oc = out_channel(layout, tj - 4, ti - 4, 4, 9, G::S2);
+          f32x4* prow = reinterpret_cast<f32x4*>(lds) + (oc * G::R + r) * G::PRQ;
+          if constexpr (G::H16) {
+            // one quad per lane; odd segment blocks XOR 4 so the two blocks sharing a
+            // ds_write_b128 lane group (8 consecutive lanes) hit disjoint 16-B slots
+            f16x8 v;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = (_Float16)epi_act(acc[ti][e], epi.slope);  // :84
-          prow[seg ^ (4 * (blk & 1))] = __builtin_bit_cast(f32x4, v);
-        } else {
+            for (int e = 0; e < 8; ++e)
+              v[e] = (_Float16)(ACT ? epi_act(acc[ti][e], epi.slope) : acc[ti][e]);
+            prow[seg ^ (4 * (blk & 1))] = __builtin_bit_cast(f32x4, v);
+          } else {
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            f32x4 v;
+            for (int h = 0; h < 2; ++h) {
+              f32x4 v;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = epi_act(acc[ti][4 * h + e], epi.slope);  // :84
-            // odd segment blocks swap their two quads: the two blocks sharing a
-            // ds_write_b128 lane group then hit disjoint 16-B slots
-            prow[2 * seg + (h ^ (blk & 1))] = v;
+              for (int e = 0; e < 4; ++e)
+                v[e] = ACT ? epi_act(acc[ti][4 * h + e], epi.slope) : acc[ti][4 * h + e];
+              // odd segment blocks swap their two quads: the two blocks sharing a
+              // ds_write_b128 lane group then hit disjoint 16-B slots
+              prow[2 * seg + (h ^ (blk & 1))] = v;
+            }
           }
         }
-      }
+      };
+      if (epi.slope == 1.f)
+        park(std::false_type{});
+      else
+        park(std::true_type{});
     }
   }
   if (wave == G::NWC) __builtin_amdgcn_s_barrier();  // the loader's side of the park barrier
