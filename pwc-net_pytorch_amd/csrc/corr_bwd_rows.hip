@@ -49,6 +49,7 @@ struct Geo {
   int nld;   // staging load items per chunk: ck * (R + 8) * (W / 4 if VEC else W)
   int cps;   // channels per slice (grid.y), a multiple of ck
   int lw;    // load items per staged row: W / 4 (VEC) or W
+  int g2v;   // VEC: gradient 2's gO values from aligned quads (else dword loads)
   float inv_lw, inv_NR, inv_I, inv_S, inv_R;
 };
 
@@ -139,6 +140,21 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
         gv[ti][1] = q ? a.w : a.z;
         gv[ti][2] = q ? c4.y : c4.x;
         gv[ti][3] = q ? c4.w : c4.z;
+      } else if (VEC && g.g2v) {
+        // raster columns 2*X0 + q + 2kk (kk = 0..3) from three aligned quads [b, b + 12);
+        // b = 2*X0 - 2*(ti & 1).  X0 < 0 only for ti >= 5, so rowoff + b stays >= 0 (the
+        // quads then start in the previous plane's data, masked below)
+        const int sh = 2 * (ti & 1);
+        const uint32_t o = rok ? (rowoff + 2 * X0 - sh) * 4u : kOOB;
+        const f32x4 a = ld4(rsg, o), bq = ld4(rsg, o + 16u), c4 = ld4(rsg, o + 32u);
+        const float w12[12] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int X = X0 + kk;
+          const bool ok = X >= 0 && X < whq;
+          const float v = q ? w12[sh + 2 * kk + 1] : w12[sh + 2 * kk];
+          gv[ti][kk] = ok ? v : 0.f;
+        }
       } else {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
@@ -324,6 +340,7 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
     if (g.G == 1) return hipErrorNotSupported;
   }
   g.lw = vec ? W / 4 : W;
+  g.g2v = debug_knob("bwd_g2v", 1);
   g.nld = g.ck * (R + 8) * g.lw;
   // channel slices (grid.y) up to one workgroup per CU over both gradients (grid.z): the
   // slices of a band are independent (every gradient element is one channel's) but each
