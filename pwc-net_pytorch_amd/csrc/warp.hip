@@ -541,8 +541,10 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
     // wide rows (l4: 96 x 112 at 384 x 448) take 16-channel tile groups and two channel groups
     // in warp_bwd_flow: 55.3 -> 42.8 us at l4; narrower levels measured best at the defaults
     // (profiles/r02d_bwd_knobs.txt)
+    // (with the per-wave list build, 16 x 16 tiles beat 8 x 32 at l4: 36.5 -> 34.5 us; l3 stays
+    // at 8 x 32, 23.3 against 26.0 -- profiles/r02e_warp_bwd_modes.txt)
     const bool wide = W >= 96;
-    const int tv = debug_knob("warp_tiles", wide ? 2 : 0);
+    const int tv = debug_knob("warp_tiles", wide ? 6 : 0);
     int th = 8, tw = 32;
     if (C > 0) {
       hipError_t e = hipSuccess;
