@@ -16,14 +16,16 @@ with its status; under an outer launcher ``--gpus`` must equal WORLD_SIZE.  At N
 broadcasts the Net harness's weights (pwcnet_amd/net.py; SURVEY §8e's startup broadcast) and
 every rank checks it received them.
 
-Timed region: every step replays the hipGraph of its buffer set (warp + correlation at l0..l3
-and the l4 warp, all direct C-ABI calls on buffers bound once per set) and then launches the
-l4 correlation -- the dominant kernel, priced for the roofline -- through the C ABI with
-hipExtLaunchKernel start/stop events (pwc_time_next_corr), so that kernel's duration is
-measured live in every timed step on the stream it runs on.  (HIP refuses external
-event-record nodes in a capture, so a captured l4 launch could not carry events; the
-comparison mode ``--timing graph-all`` captures the whole step in one graph, without kernel
-events: it measures the eager launch's share of the step.)
+Timed region: every step launches warp + correlation at l0..l3 and the l4 warp as direct
+C-ABI calls on buffers bound once per set (the ctypes arguments are built once, so a launch
+costs one foreign call), then the l4 correlation -- the dominant kernel, priced for the
+roofline -- through the C ABI with hipExtLaunchKernel start/stop events (pwc_time_next_corr),
+so that kernel's duration is measured live in every timed step on the stream it runs on.  On
+ROCm this 8-kernel step runs faster as plain launches than replayed from a hipGraph (which
+also makes the event-armed launch dearer), so graphs are comparison modes:
+``--timing graph-eager`` replays a per-set graph of l0..l3 and the l4 warp before the same
+event-armed launch; ``--timing graph-all`` captures the whole step in one graph, without
+kernel events (HIP refuses external event-record nodes in a capture).
 Inputs rotate over enough buffer sets (> 2x the 256 MiB Infinity Cache) that each step reads
 them from HBM.  After timing, a replay self-check re-runs one step with every output poisoned
 (NaN) and compares all five levels bit for bit with a fresh eager computation, and a shard
@@ -100,11 +102,13 @@ def parse_args(argv=None):
     ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-graph", action="store_true", help="eager launches (timing 'eager')")
-    ap.add_argument("--timing", default="graph-eager", choices=["graph-eager", "graph-all"],
-                    help="graph-eager: per-set graphs of l0..l3 + the l4 warp, then an eager "
-                         "event-armed l4 correlation; graph-all (comparison only): the whole "
-                         "step in one graph, no kernel events")
+    ap.add_argument("--no-graph", action="store_true", help="same as --timing eager")
+    ap.add_argument("--timing", default="eager", choices=["eager", "graph-eager", "graph-all"],
+                    help="eager (default): every kernel a direct C-ABI launch on pre-built "
+                         "arguments, the l4 correlation event-armed; graph-eager: per-set graphs "
+                         "of l0..l3 + the l4 warp, then the event-armed l4 correlation; "
+                         "graph-all (comparison only): the whole step in one graph, no kernel "
+                         "events")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = launcher rehearsal over gloo with a torch-CPU stand-in op")
     ap.add_argument("--fused-levels", default="0,1",
@@ -210,6 +214,55 @@ class HipPass:
     def sp(self):
         """The CURRENT stream (torch.cuda.graph captures on its own side stream)."""
         return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def prepare(self, s):
+        """Pre-built (function, ctypes arguments) lists of pre() and of the l4 correlation on
+        the current stream, so an eager step is a loop of foreign calls with nothing to convert
+        (the Python side of a launch otherwise costs about as much as the kernel at l0-l2)."""
+        L, P, p = self.lib, self.P, self._p
+        sp = self.sp
+        c_int = ctypes.c_int
+        calls = []
+        for l, lv in enumerate(s):
+            B, C, h, w = lv["x1"].shape
+            dims = [c_int(B), c_int(C), c_int(h), c_int(w)]
+            cp = [c_int(v) for v in P]
+            if l == len(s) - 1 or l not in self.fused:
+                calls.append((L.pwc_warp_forward, (p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]),
+                                                   *dims, c_int(self.dcode), sp), f"warp l{l}"))
+            if l == len(s) - 1:
+                continue
+            if l in self.fused:
+                calls.append((L.pwc_warp_corr_forward,
+                              (p(lv["x1"]), p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]),
+                               p(lv["corr"]), *dims, *cp, c_int(1), c_int(self.dcode),
+                               p(lv["ws"]), ctypes.c_size_t(lv["nws"]), sp), f"level {l}"))
+            else:
+                calls.append((L.pwc_corr_forward_ws,
+                              (p(lv["x1"]), p(lv["x2w"]), p(lv["corr"]), *dims, *cp, c_int(1),
+                               c_int(self.dcode), p(lv["ws"]), ctypes.c_size_t(lv["nws"]), sp),
+                              f"level {l}"))
+        lv = s[-1]
+        B, C, h, w = lv["x1"].shape
+        corr = (L.pwc_corr_forward, (p(lv["x1"]), p(lv["x2w"]), p(lv["corr"]), c_int(B), c_int(C),
+                                     c_int(h), c_int(w), *[c_int(v) for v in P], c_int(1),
+                                     c_int(self.dcode), sp))
+        return calls, corr
+
+    def step_prepared(self, prep, events=None):
+        """One eager step from prepare()'s lists; ``events`` arms the l4 correlation."""
+        calls, (cfn, cargs) = prep
+        for fn, args, what in calls:
+            ret = fn(*args)
+            if ret != 1:
+                self._lib.check(ret, "bench " + what)
+        if events is not None:
+            self._lib.check(self.lib.pwc_time_next_corr(ctypes.c_void_p(events[0].cuda_event),
+                                                        ctypes.c_void_p(events[1].cuda_event)),
+                            "bench")
+        ret = cfn(*cargs)
+        if ret != 1:
+            self._lib.check(ret, "bench corr_l4")
 
     @staticmethod
     def _p(t):
@@ -576,7 +629,7 @@ def main(argv=None):
         gen = torch.Generator(device=dev).manual_seed(1234 + rank)
         sets = [random_set(shapes, B, dev, dtype, gen) for _ in range(nsets)]
 
-    graphs = []
+    graphs, preps = [], []
     timing = "cpu" if cpu else ("eager" if args.no_graph else args.timing)
     if not cpu:
         for s in sets:
@@ -609,6 +662,10 @@ def main(argv=None):
                 with torch.cuda.graph(g, pool=pool):
                     pass_.pre(s)
                 graphs.append(g)
+        else:
+            # eager: every launch a direct C-ABI call on pre-built ctypes arguments (on ROCm
+            # this step runs faster as plain launches than as graph replays)
+            preps = [pass_.prepare(s) for s in sets]
         torch.cuda.synchronize(dev)
 
     def step(i, ev=None):
@@ -618,6 +675,9 @@ def main(argv=None):
             return
         if timing == "graph-all":
             graphs[i % nsets].replay()
+            return
+        if preps:
+            pass_.step_prepared(preps[i % nsets], ev)
             return
         if graphs:
             graphs[i % nsets].replay()
@@ -638,6 +698,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i, None if cpu else evs[i])
+    issued = time.perf_counter() - t0  # host time to issue the steps (GPU-bound if << elapsed)
     sync()
     if world > 1:
         dist.barrier()
@@ -683,6 +744,7 @@ def main(argv=None):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "host_issue_ms_per_step": round(issued / args.steps * 1e3, 5),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
