@@ -22,7 +22,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from pwcnet_amd.ops import corr_backward, corr_forward, warp_backward, warp_forward  # noqa: E402
+from pwcnet_amd.ops import (corr_backward, corr_forward, warp_backward,  # noqa: E402
+                            warp_corr_forward, warp_forward)
 
 
 def main():
@@ -32,7 +33,10 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--height", type=int, default=384)
     ap.add_argument("--width", type=int, default=448)
+    ap.add_argument("--fused-levels", default="0,1",
+                    help="levels whose forward runs as one WarpCorrelation launch (as bench.py)")
     args = ap.parse_args()
+    fused = {int(v) for v in args.fused_levels.split(",") if v.strip()}
     dev = torch.device("cuda:0")
     B = args.batch
     shapes = bench.level_shapes(args.height, args.width)
@@ -50,9 +54,13 @@ def main():
         sets.append(s)
 
     def one(s):
-        for lv in s:
-            x2w = warp_forward(lv["x2"], lv["fl"])
-            lv["corr"] = corr_forward(lv["x1"], x2w, **bench.CORR_ARGS)
+        for l, lv in enumerate(s):
+            if l in fused:  # model.py:80-83 as one WarpCorrelation launch (emits x2_warp too)
+                lv["corr"], x2w = warp_corr_forward(lv["x1"], lv["x2"], lv["fl"],
+                                                    **bench.CORR_ARGS)
+            else:
+                x2w = warp_forward(lv["x2"], lv["fl"])
+                lv["corr"] = corr_forward(lv["x1"], x2w, **bench.CORR_ARGS)
             g1, g2w = corr_backward(lv["x1"], x2w, lv["gc"], **bench.CORR_ARGS)
             lv["g1"] = g1
             lv["gx2"], lv["gfl"] = warp_backward(lv["x2"], lv["fl"], g2w)
@@ -84,6 +92,7 @@ def main():
         "data": "synthetic (randn features and cost-volume gradients, N(0,2^2) flows)",
         "config": {"workload": "BASELINE config 5: B=8 384x448 training step of the hot path",
                    "batch": B, "levels": [list(x) for x in shapes], "graph": True,
+                   "fused_levels": sorted(fused),
                    "buffer_sets": nsets}}), flush=True)
 
 
