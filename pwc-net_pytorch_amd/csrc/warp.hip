@@ -508,11 +508,13 @@ hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int
   hipLaunchKernelGGL((warp_fwd_kernel<T, CB, NG, XCD>),                                       \
                      dim3(gx, (unsigned)((C + CB * NG - 1) / (CB * NG))), dim3(256), 0, stream, \
                      (const T*)x, (const T*)flow, (T*)out, B, C, H, W, halfx, halfy)
-  // fp16 storage on large grids: a thread walks 4 groups of 4 channels (its gathers of the
-  // next group in flight while one is blended) -- config-4 Sintel l4 34.0 -> 27.6 us, l3 18.9
-  // -> 15.7, l2 9.2 -> 8.6 (B=16); fp32 measured best at one group of 4 (r02d_warp_cb_sweep)
+  // fp16 storage on large grids: a thread walks 4 groups of channels (its gathers of the next
+  // group in flight while one is blended) -- config-4 Sintel l4 34.0 -> 27.6 us, l3 18.9 ->
+  // 15.7, l2 9.2 -> 8.6 (B=16) with groups of 4; groups of 2 (more threads) another 3-7 %:
+  // l4 30.3 -> 28.0, l3 16.6 -> 16.2, l2 8.67 -> 8.42 (profiles/r02e_warp_fp16_cfg.txt); fp32
+  // measured best at one group of 4 (r02d_warp_cb_sweep)
   int cfg = warp_cfg();
-  if (cfg == 0 && sizeof(T) == 2 && npix >= 16384) cfg = 7;
+  if (cfg == 0 && sizeof(T) == 2 && npix >= 16384) cfg = 9;
   switch (cfg) {
     case 1: PWC_WARP_LAUNCH(8, 1, false); break;
     case 2: PWC_WARP_LAUNCH(2, 1, false); break;
