@@ -766,9 +766,14 @@ static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C
                                                     stream);
     }
   }
-  switch (debug_knob("stream_cfg", 0)) {  // measurement variants (CC, NS)
+  // stride-1 displacements (Corr4, CostVolumeLayer): the 4 x 4 ring needs more than the 256
+  // VGPRs (~640 spilled to scratch), 2 x 4 none, at the same time (l4 16.9-17.0 us against
+  // 16.9-17.3 over 300 launches each; profiles/r02e_corr4_ring.txt)
+  const int dcfg = S2 == 1 ? 2 : 0;
+  switch (debug_knob("stream_cfg", dcfg)) {  // measurement variants (CC, NS)
     case 2: return launch<Geo<T, S2, 3, TWP, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
     case 8: return launch<Geo<T, S2, 3, TWP, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+    case 4: return launch<Geo<T, S2, 3, TWP, 4, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
     default: return launch<Geo<T, S2, 3, TWP, 4, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
   }
 }
