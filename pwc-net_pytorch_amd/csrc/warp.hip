@@ -251,12 +251,12 @@ __device__ __forceinline__ bool bwd_in_window(int py, int px, int cy, int cx, in
          px < tx0 + tw + kBwdM;
 }
 
-template <int TW, int CC, int MODE = 0>
-__global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict__ flow,
-                                                         const float* __restrict__ gout,
-                                                         float* __restrict__ gx, int C, int H,
-                                                         int W, float halfx, float halfy,
-                                                         int ntx) {
+template <int TW, int CC, int MODE>
+__device__ __forceinline__ void warp_bwd_gx_body(const float* __restrict__ flow,
+                                                 const float* __restrict__ gout,
+                                                 float* __restrict__ gx, int C, int H, int W,
+                                                 float halfx, float halfy, int ntx, int bx,
+                                                 int by, int bz) {
   constexpr int TH = 256 / TW, M = kBwdM;
   constexpr int WW = TW + 2 * M, NCAND = (TH + 2 * M) * WW, K = (NCAND + 255) / 256;
   constexpr int MAXL = 4 * NCAND;
@@ -266,8 +266,8 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
   __shared__ unsigned lpix[MAXL];
   __shared__ float lw[MAXL];
   const int t = threadIdx.x;
-  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  const int n = blockIdx.y, c0 = blockIdx.z * CC;
+  const int tx = bx % ntx, ty = bx / ntx;
+  const int n = by, c0 = bz * CC;
   const int y0 = ty * TH, x0 = tx * TW;
   const unsigned plane = (unsigned)(H * W);
   const int cw = WAVEC ? (t >> 6) * 256 : 0;  // this wave's counter row
@@ -395,23 +395,33 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
     if (i < cn) o[(unsigned)i * plane] = acc[i];
 }
 
+template <int TW, int CC, int MODE = 0>
+__global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict__ flow,
+                                                         const float* __restrict__ gout,
+                                                         float* __restrict__ gx, int C, int H,
+                                                         int W, float halfx, float halfy,
+                                                         int ntx) {
+  warp_bwd_gx_body<TW, CC, MODE>(flow, gout, gx, C, H, W, halfx, halfy, ntx, blockIdx.x,
+                                 blockIdx.y, blockIdx.z);
+}
+
 // grad_flow per pixel + the corners warp_bwd_gx_lists left out.  A block holds 256 / NG
 // pixels x NG channel groups (lanes of a wave = consecutive pixels of one group); group g
 // takes channels [g*cpg, (g+1)*cpg) and the NG partial sums meet in LDS in group order
 // (deterministic; NG = 1 is ATen's channel loop order).
-template <int CB, int NG, bool PAIRS = false>
-__global__ __launch_bounds__(256) void warp_bwd_flow(const float* __restrict__ x,
-                                                     const float* __restrict__ flow,
-                                                     const float* __restrict__ gout,
-                                                     float* __restrict__ gx,
-                                                     float* __restrict__ gflow, int B, int C,
-                                                     int H, int W, float halfx, float halfy,
-                                                     int cpg, int th, int tw) {
+template <int CB, int NG, bool PAIRS>
+__device__ __forceinline__ void warp_bwd_flow_body(const float* __restrict__ x,
+                                                   const float* __restrict__ flow,
+                                                   const float* __restrict__ gout,
+                                                   float* __restrict__ gx,
+                                                   float* __restrict__ gflow, int B, int C,
+                                                   int H, int W, float halfx, float halfy,
+                                                   int cpg, int th, int tw, unsigned blk) {
   constexpr int PX = 256 / NG;
   __shared__ float red[NG > 1 ? 2 * 256 : 1];
   const unsigned plane = (unsigned)(H * W);
   const int grp = threadIdx.x / PX, pl = threadIdx.x - grp * PX;
-  const unsigned idx = xcd_remap(blockIdx.x, gridDim.x) * (unsigned)PX + pl;
+  const unsigned idx = blk * (unsigned)PX + pl;
   const bool live = idx < (unsigned)B * plane;
   if (NG == 1 && !live) return;
   const unsigned idc = live ? idx : 0u;  // idle lanes of the last block sample pixel 0
@@ -491,6 +501,41 @@ __global__ __launch_bounds__(256) void warp_bwd_flow(const float* __restrict__ x
   gflow[(2 * n + 1) * plane + pix] = (giy * my) / halfy;
 }
 
+template <int CB, int NG, bool PAIRS = false>
+__global__ __launch_bounds__(256) void warp_bwd_flow(const float* __restrict__ x,
+                                                     const float* __restrict__ flow,
+                                                     const float* __restrict__ gout,
+                                                     float* __restrict__ gx,
+                                                     float* __restrict__ gflow, int B, int C,
+                                                     int H, int W, float halfx, float halfy,
+                                                     int cpg, int th, int tw) {
+  warp_bwd_flow_body<CB, NG, PAIRS>(x, flow, gout, gx, gflow, B, C, H, W, halfx, halfy, cpg, th,
+                                    tw, (unsigned)xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// Images that fit one grad_x tile (l0 / l1): the two kernels in ONE launch, side by side --
+// the first ngx workgroups build the lists and gather grad_x, the rest compute grad_flow.
+// With the tile covering the whole image every in-image corner lies in its tile's window, so
+// there are no far corners and no atomics, and the two halves are independent.
+template <int TW, int CC, int MODE, int CB, int NG, bool PAIRS>
+__global__ __launch_bounds__(256) void warp_bwd_small(const float* __restrict__ x,
+                                                      const float* __restrict__ flow,
+                                                      const float* __restrict__ gout,
+                                                      float* __restrict__ gx,
+                                                      float* __restrict__ gflow, int B, int C,
+                                                      int H, int W, float halfx, float halfy,
+                                                      int cpg, int ngx, int ncg) {
+  const int b = blockIdx.x;
+  if (b < ngx) {
+    warp_bwd_gx_body<TW, CC, MODE>(flow, gout, gx, C, H, W, halfx, halfy, 1, 0, b / ncg,
+                                   b % ncg);
+  } else {
+    const int nf = (int)gridDim.x - ngx;
+    warp_bwd_flow_body<CB, NG, PAIRS>(x, flow, gout, gx, gflow, B, C, H, W, halfx, halfy, cpg,
+                                      256 / TW, TW, (unsigned)xcd_remap(b - ngx, nf));
+  }
+}
+
 // knob warp_cfg selects a (channels per group, groups per thread) variant for measurement:
 // 0 = 4 channels per thread, XCD-grouped pixel blocks (default), 1 = 8, 2 = 2,
 // 3 = 4 without XCD grouping, 4 = 2 grouped, 5 = 8 grouped.
@@ -546,6 +591,29 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
     // (with the per-wave list build, 16 x 16 tiles beat 8 x 32 at l4: 36.5 -> 34.5 us; l3 stays
     // at 8 x 32, 23.3 against 26.0 -- profiles/r02e_warp_bwd_modes.txt)
     const bool wide = W >= 96;
+    // images inside one grad_x tile (l0 6 x 7 in 8 x 32, l1 12 x 14 in 16 x 16): grad_x and
+    // grad_flow in one merged launch (warp_bwd_small; knob warp_bwd_small=0 for two launches)
+    if (C > 0 && debug_knob("warp_bwd_small", 1) && debug_knob("warp_tiles", -1) < 0 &&
+        debug_knob("wbg_mode", 6) == 6) {
+      int ng = 1;
+      while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
+      const int tws = (H <= 8 && W <= 32) ? 32 : (H <= 16 && W <= 16) ? 16 : 0;
+      if (tws && ng == 16) {
+        const int cc = tws == 32 ? 8 : 16, ncg = (C + cc - 1) / cc, ngx = B * ncg;
+        const int cpg = (C + ng - 1) / ng;
+        const unsigned nflow = (unsigned)((npix * ng + 255) / 256);
+        const dim3 grid((unsigned)ngx + nflow);
+        if (tws == 32)
+          hipLaunchKernelGGL((warp_bwd_small<32, 8, 6, 8, 16, true>), grid, dim3(256), 0, stream,
+                             (const float*)x, (const float*)flow, (const float*)gout, (float*)gx,
+                             (float*)gflow, B, C, H, W, halfx, halfy, cpg, ngx, ncg);
+        else
+          hipLaunchKernelGGL((warp_bwd_small<16, 16, 6, 8, 16, true>), grid, dim3(256), 0,
+                             stream, (const float*)x, (const float*)flow, (const float*)gout,
+                             (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy, cpg, ngx, ncg);
+        return hipGetLastError();
+      }
+    }
     const int tv = debug_knob("warp_tiles", wide ? 6 : 0);
     int th = 8, tw = 32;
     if (C > 0) {

@@ -224,6 +224,34 @@ def test_warp_backward_tiles_and_outliers(scale):
     np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
 
 
+@pytest.mark.parametrize("shape", [(2, 192, 6, 7), (2, 128, 12, 14)])
+@pytest.mark.parametrize("scale", [0.0, 3.0, 25.0])
+def test_warp_backward_small_images_one_launch(shape, scale):
+    """l0 / l1-sized images fit one grad_x tile: grad_x lists and grad_flow run as one merged
+    launch (warp_bwd_small) -- against the oracle for zero, moderate and far (mostly
+    out-of-image) flows, repeatable bit for bit, and equal to the two-launch path up to the
+    summation order (l1 takes 16 x 16 tiles there, 8 x 32 in two launches)."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import warp_backward
+    B, C, H, W = shape
+    rng = np.random.default_rng(29)
+    x, g = _rand(rng, B, C, H, W), _rand(rng, B, C, H, W)
+    f = (rng.standard_normal((B, 2, H, W)) * scale).astype(np.float32)
+    gx, gf = warp_backward(_t(x), _t(f), _t(g))
+    rx, rf = O.warp_backward(x, f, g)
+    np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
+    gx1, gf1 = warp_backward(_t(x), _t(f), _t(g))
+    assert torch.equal(gx, gx1) and torch.equal(gf, gf1)
+    _lib.set_debug("warp_bwd_small=0")
+    try:
+        gx2, gf2 = warp_backward(_t(x), _t(f), _t(g))
+    finally:
+        _lib.set_debug("")
+    np.testing.assert_allclose(_np(gx), _np(gx2), rtol=1e-6, atol=1e-6)
+    assert torch.equal(gf, gf2)  # same flow kernel, same channel groups
+
+
 @pytest.mark.parametrize("shape", [(2, 32, 96, 112), (2, 13, 37, 70)])
 def test_warp_backward_converging_lists_repeatable(shape):
     """Flows pulling every pixel toward a few sinks (within the candidate margin, so no
