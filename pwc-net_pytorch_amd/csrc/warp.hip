@@ -409,7 +409,9 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_lists(const float* __restrict
 // pixels x NG channel groups (lanes of a wave = consecutive pixels of one group); group g
 // takes channels [g*cpg, (g+1)*cpg) and the NG partial sums meet in LDS in group order
 // (deterministic; NG = 1 is ATen's channel loop order).
-template <int CB, int NG, bool PAIRS>
+// NOFAR: the far corners are left to warp_bwd_far (a merged launch cannot order its atomics
+// after the grad_x tiles' plain stores)
+template <int CB, int NG, bool PAIRS, bool NOFAR = false>
 __device__ __forceinline__ void warp_bwd_flow_body(const float* __restrict__ x,
                                                    const float* __restrict__ flow,
                                                    const float* __restrict__ gout,
@@ -443,7 +445,7 @@ __device__ __forceinline__ void warp_bwd_flow_body(const float* __restrict__ x,
   const bool o01 = k.m01 != 0.f && !bwd_in_window(py, px, b.y0, b.x0 + 1, th, tw);
   const bool o10 = k.m10 != 0.f && !bwd_in_window(py, px, b.y0 + 1, b.x0, th, tw);
   const bool o11 = k.m11 != 0.f && !bwd_in_window(py, px, b.y0 + 1, b.x0 + 1, th, tw);
-  const bool outl = o00 || o01 || o10 || o11;
+  const bool outl = !NOFAR && (o00 || o01 || o10 || o11);
   float gix = 0.f, giy = 0.f;
   const int cs = grp * cpg, ce = live ? min(C, cs + cpg) : cs;
   for (int c0 = cs; c0 < ce; c0 += CB) {
@@ -536,6 +538,62 @@ __global__ __launch_bounds__(256) void warp_bwd_small(const float* __restrict__ 
   }
 }
 
+// Multi-tile images: grad_x tiles and grad_flow side by side in one launch (both are gather
+// kernels far below the chip's memory rate, so together they fill it better), the far corners
+// in a small pass after it (warp_bwd_far).
+template <int TW, int CC, int MODE, int CB, int NG, bool PAIRS>
+__global__ __launch_bounds__(256) void warp_bwd_merged(const float* __restrict__ x,
+                                                       const float* __restrict__ flow,
+                                                       const float* __restrict__ gout,
+                                                       float* __restrict__ gx,
+                                                       float* __restrict__ gflow, int B, int C,
+                                                       int H, int W, float halfx, float halfy,
+                                                       int cpg, int ntx, int ntiles, int ngx) {
+  const int b = blockIdx.x;
+  if (b < ngx) {
+    const int rest = b / ntiles;
+    warp_bwd_gx_body<TW, CC, MODE>(flow, gout, gx, C, H, W, halfx, halfy, ntx, b % ntiles,
+                                   rest % B, rest / B);
+  } else {
+    const int nf = (int)gridDim.x - ngx;
+    warp_bwd_flow_body<CB, NG, PAIRS, true>(x, flow, gout, gx, gflow, B, C, H, W, halfx, halfy,
+                                            cpg, 256 / TW, TW, (unsigned)xcd_remap(b - ngx, nf));
+  }
+}
+
+// The corners warp_bwd_merged's tiles left out (sample point beyond ~kBwdM pixels of its
+// corner's tile): one thread per pixel, global atomics as ATen's scatter, after the tiles.
+__global__ __launch_bounds__(256) void warp_bwd_far(const float* __restrict__ flow,
+                                                    const float* __restrict__ gout,
+                                                    float* __restrict__ gx, int B, int C, int H,
+                                                    int W, float halfx, float halfy, int th,
+                                                    int tw) {
+  const unsigned plane = (unsigned)(H * W);
+  const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= (unsigned)B * plane) return;
+  const unsigned n = idx / plane, pix = idx - n * plane;
+  const int py = (int)(pix / (unsigned)W), px = (int)pix - py * W;
+  const float u = flow[(2 * n + 0) * plane + pix];
+  const float v = flow[(2 * n + 1) * plane + pix];
+  const Bilinear b = bilinear(src_coord(u, px, W, halfx), src_coord(v, py, H, halfy), H, W);
+  const Corners k = corners(b, H, W);
+  const bool o00 = k.m00 != 0.f && !bwd_in_window(py, px, b.y0, b.x0, th, tw);
+  const bool o01 = k.m01 != 0.f && !bwd_in_window(py, px, b.y0, b.x0 + 1, th, tw);
+  const bool o10 = k.m10 != 0.f && !bwd_in_window(py, px, b.y0 + 1, b.x0, th, tw);
+  const bool o11 = k.m11 != 0.f && !bwd_in_window(py, px, b.y0 + 1, b.x0 + 1, th, tw);
+  if (!(o00 || o01 || o10 || o11)) return;
+  const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;
+  const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
+  for (int c = 0; c < C; ++c) {
+    const float g = gout[((unsigned)(n * C + c)) * plane + pix];
+    float* q = gx + ((unsigned)(n * C + c)) * plane;
+    if (o00) atomicAdd(q + k.i00, g * w00);
+    if (o01) atomicAdd(q + k.i01, g * w01);
+    if (o10) atomicAdd(q + k.i10, g * w10);
+    if (o11) atomicAdd(q + k.i11, g * w11);
+  }
+}
+
 // knob warp_cfg selects a (channels per group, groups per thread) variant for measurement:
 // 0 = 4 channels per thread, XCD-grouped pixel blocks (default), 1 = 8, 2 = 2,
 // 3 = 4 without XCD grouping, 4 = 2 grouped, 5 = 8 grouped.
@@ -615,6 +673,45 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
       }
     }
     const int tv = debug_knob("warp_tiles", wide ? 6 : 0);
+    // grad_x tiles and grad_flow in one launch + the far-corner pass (knob warp_bwd_merge)
+    if (C > 0 && debug_knob("warp_bwd_merge", 1) && debug_knob("wbg_mode", 6) == 6 &&
+        debug_knob("wbf_pairs", 1) && (tv == 0 || tv == 6)) {
+      int ng = 1;
+      while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
+      if (wide && ng == 1 && C >= 32) ng = 2;
+      if (const int k = debug_knob("warp_bwd_ng", 0)) ng = k;
+      const int TWm = tv == 6 ? 16 : 32, CCm = tv == 6 ? 16 : 8, THm = 256 / TWm;
+      const int ntx = (W + TWm - 1) / TWm, nty = (H + THm - 1) / THm, ntiles = ntx * nty;
+      const int ngx = ntiles * B * ((C + CCm - 1) / CCm);
+      const int cpg = (C + ng - 1) / ng;
+      const unsigned nflow = (unsigned)((npix * ng + 255) / 256);
+      // only where both halves fit about one round of the chip together: l2 17.5 -> 13.1 us;
+      // l3 (1104 workgroups) 22.8 -> 29.7 and l4 (1344) 34.8 -> 39.1 measured slower
+      // (profiles/r02e_warp_bwd_small.txt)
+      bool done = (long long)ngx + nflow > 512;
+#define PWC_MERGED(TVV, TW_, CC_, NG_)                                                         \
+  if (!done && tv == TVV && ng == NG_) {                                                       \
+    hipLaunchKernelGGL((warp_bwd_merged<TW_, CC_, 6, 8, NG_, true>), dim3((unsigned)ngx + nflow), \
+                       dim3(256), 0, stream, (const float*)x, (const float*)flow,              \
+                       (const float*)gout, (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy, \
+                       cpg, ntx, ntiles, ngx);                                                 \
+    done = true;                                                                               \
+  }
+      PWC_MERGED(0, 32, 8, 8)
+      PWC_MERGED(0, 32, 8, 4)
+      PWC_MERGED(0, 32, 8, 2)
+      PWC_MERGED(6, 16, 16, 2)
+      PWC_MERGED(6, 16, 16, 1)
+#undef PWC_MERGED
+      if (done && (long long)ngx + nflow <= 512) {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(warp_bwd_far, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream,
+                           (const float*)flow, (const float*)gout, (float*)gx, B, C, H, W, halfx,
+                           halfy, THm, TWm);
+        return hipGetLastError();
+      }
+    }
     int th = 8, tw = 32;
     if (C > 0) {
       hipError_t e = hipSuccess;

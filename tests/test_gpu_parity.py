@@ -224,13 +224,15 @@ def test_warp_backward_tiles_and_outliers(scale):
     np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
 
 
-@pytest.mark.parametrize("shape", [(2, 192, 6, 7), (2, 128, 12, 14)])
+@pytest.mark.parametrize("shape", [(2, 192, 6, 7), (2, 128, 12, 14), (2, 96, 24, 28)])
 @pytest.mark.parametrize("scale", [0.0, 3.0, 25.0])
 def test_warp_backward_small_images_one_launch(shape, scale):
     """l0 / l1-sized images fit one grad_x tile: grad_x lists and grad_flow run as one merged
-    launch (warp_bwd_small) -- against the oracle for zero, moderate and far (mostly
-    out-of-image) flows, repeatable bit for bit, and equal to the two-launch path up to the
-    summation order (l1 takes 16 x 16 tiles there, 8 x 32 in two launches)."""
+    launch (warp_bwd_small); l2-sized grids run the tiles and grad_flow as one launch plus the
+    far-corner pass (warp_bwd_merged + warp_bwd_far) -- against the oracle for zero, moderate
+    and far (mostly out-of-image) flows, repeatable bit for bit when no far corner exists, and
+    equal to the separate launches up to the summation order (l1 takes 16 x 16 tiles there,
+    8 x 32 in two launches)."""
     from pwcnet_amd import _lib
     from pwcnet_amd.ops import warp_backward
     B, C, H, W = shape
@@ -242,14 +244,16 @@ def test_warp_backward_small_images_one_launch(shape, scale):
     np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
     gx1, gf1 = warp_backward(_t(x), _t(f), _t(g))
-    assert torch.equal(gx, gx1) and torch.equal(gf, gf1)
-    _lib.set_debug("warp_bwd_small=0")
+    assert torch.equal(gf, gf1)
+    if scale < 8:  # far corners go through atomics (ATen's order-free scatter)
+        assert torch.equal(gx, gx1)
+    _lib.set_debug("warp_bwd_small=0,warp_bwd_merge=0")
     try:
         gx2, gf2 = warp_backward(_t(x), _t(f), _t(g))
     finally:
         _lib.set_debug("")
     np.testing.assert_allclose(_np(gx), _np(gx2), rtol=1e-6, atol=1e-6)
-    assert torch.equal(gf, gf2)  # same flow kernel, same channel groups
+    assert torch.equal(gf, gf2)  # same grad_flow code, same channel groups
 
 
 @pytest.mark.parametrize("shape", [(2, 32, 96, 112), (2, 13, 37, 70)])
