@@ -674,8 +674,12 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
     }
     const int tv = debug_knob("warp_tiles", wide ? 6 : 0);
     // grad_x tiles and grad_flow in one launch + the far-corner pass (knob warp_bwd_merge)
+    // merged tiles: 16 x 16 from 48-px rows (l3: 720 workgroups, 23.3 -> 21.7 us against the
+    // two launches of 8 x 32 tiles), else 8 x 32 (l2)
+    const int tvm = debug_knob("warp_tiles", W >= 48 ? 6 : 0);
     if (C > 0 && debug_knob("warp_bwd_merge", 1) && debug_knob("wbg_mode", 6) == 6 &&
-        debug_knob("wbf_pairs", 1) && (tv == 0 || tv == 6)) {
+        debug_knob("wbf_pairs", 1) && (tvm == 0 || tvm == 6)) {
+      const int tv = tvm;
       int ng = 1;
       while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
       if (wide && ng == 1 && C >= 32) ng = 2;
@@ -685,10 +689,11 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
       const int ngx = ntiles * B * ((C + CCm - 1) / CCm);
       const int cpg = (C + ng - 1) / ng;
       const unsigned nflow = (unsigned)((npix * ng + 255) / 256);
-      // only where both halves fit about one round of the chip together: l2 17.5 -> 13.1 us;
-      // l3 (1104 workgroups) 22.8 -> 29.7 and l4 (1344) 34.8 -> 39.1 measured slower
-      // (profiles/r02e_warp_bwd_small.txt)
-      bool done = (long long)ngx + nflow > 512;
+      // only where both halves fit about one round of the chip together: l2 (456 workgroups)
+      // 17.5 -> 13.1 us, l3 (720) 23.3 -> 21.7; l3 with 8 x 32 tiles (1104) 22.8 -> 29.7 and
+      // l4 (1344) 34.8 -> 39.1 measured slower (profiles/r02e_warp_bwd_small.txt)
+      const long long mcap = debug_knob("warp_bwd_mcap", 800);
+      bool done = (long long)ngx + nflow > mcap;
 #define PWC_MERGED(TVV, TW_, CC_, NG_)                                                         \
   if (!done && tv == TVV && ng == NG_) {                                                       \
     hipLaunchKernelGGL((warp_bwd_merged<TW_, CC_, 6, 8, NG_, true>), dim3((unsigned)ngx + nflow), \
@@ -700,10 +705,11 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
       PWC_MERGED(0, 32, 8, 8)
       PWC_MERGED(0, 32, 8, 4)
       PWC_MERGED(0, 32, 8, 2)
+      PWC_MERGED(6, 16, 16, 4)
       PWC_MERGED(6, 16, 16, 2)
       PWC_MERGED(6, 16, 16, 1)
 #undef PWC_MERGED
-      if (done && (long long)ngx + nflow <= 512) {
+      if (done && (long long)ngx + nflow <= mcap) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(warp_bwd_far, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream,
