@@ -94,7 +94,9 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps first (default 300 on the GPU, about 30 ms at config 2: "
+                         "clocks and caches settle; 2 for --device cpu)")
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU")
     ap.add_argument("--height", type=int, default=384)
     ap.add_argument("--width", type=int, default=448)
@@ -117,7 +119,10 @@ def parse_args(argv=None):
                     help="committed PMC summary used when the live passes cannot run")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 PMC passes for roofline.traffic")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.warmup is None:
+        args.warmup = 2 if args.device == "cpu" else 300
+    return args
 
 
 def _free_port():

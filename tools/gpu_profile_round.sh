@@ -8,10 +8,10 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 cd /tmp
-timeout -k 10 400 python $R/bench.py --steps 200 --warmup 20 --cpu-seconds 10 > $OUT/bench_full.json 2> $OUT/bench_full.err || { tail $OUT/bench_full.err; exit 1; }
+timeout -k 10 400 python $R/bench.py --cpu-seconds 10 > $OUT/bench_full.json 2> $OUT/bench_full.err || { tail $OUT/bench_full.err; exit 1; }
 echo bench done
-timeout -k 10 300 python $R/bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-pmc --timing graph-all > $OUT/bench_graph_all.json 2> $OUT/bench_graph_all.err || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python $R/bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-pmc > $OUT/bench_traced.json 2> $OUT/trace.err || { tail $OUT/trace.err; exit 1; }
+timeout -k 10 300 python $R/bench.py --no-cpu-baseline --no-pmc --timing graph-all > $OUT/bench_graph_all.json 2> $OUT/bench_graph_all.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python $R/bench.py --no-cpu-baseline --no-pmc > $OUT/bench_traced.json 2> $OUT/trace.err || { tail $OUT/trace.err; exit 1; }
 echo trace done
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex corr_fwd_stream -d $OUT/pmc_$ctr -o run --output-format csv -- python $R/tools/kbench.py --levels 4 --ops corr --iters 20 > $OUT/pmc_$ctr.log 2>&1 || { tail $OUT/pmc_$ctr.log; exit 1; }
