@@ -22,6 +22,6 @@ timeout -k 10 300 python $R/tools/kbench.py --iters 40 --ops corr,warp,fused,upw
 timeout -k 10 200 python $R/tools/train_bench.py > $OUT/train.json 2> $OUT/train.err || { tail $OUT/train.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/train_trace -o run --output-format csv -- python $R/tools/train_bench.py > $OUT/train_traced.json 2> $OUT/train_trace.err || exit 1
 echo train done
-timeout -k 10 300 python $R/bench.py --dtype fp16 --batch 16 --height 448 --width 1024 --steps 100 --warmup 10 --no-cpu-baseline > $OUT/cfg4_bench.json 2> $OUT/cfg4.err || { tail $OUT/cfg4.err; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/cfg4_trace -o run --output-format csv -- python $R/bench.py --dtype fp16 --batch 16 --height 448 --width 1024 --steps 100 --warmup 10 --no-cpu-baseline --no-pmc > $OUT/cfg4_traced.json 2> $OUT/cfg4_trace.err || exit 1
+timeout -k 10 300 python $R/bench.py --dtype fp16 --batch 16 --height 448 --width 1024 --no-cpu-baseline > $OUT/cfg4_bench.json 2> $OUT/cfg4.err || { tail $OUT/cfg4.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/cfg4_trace -o run --output-format csv -- python $R/bench.py --dtype fp16 --batch 16 --height 448 --width 1024 --no-cpu-baseline --no-pmc > $OUT/cfg4_traced.json 2> $OUT/cfg4_trace.err || exit 1
 echo all done

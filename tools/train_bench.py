@@ -29,7 +29,7 @@ from pwcnet_amd.ops import (corr_backward, corr_forward, warp_backward,  # noqa:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=100)  # ~28 ms: clocks settle
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--height", type=int, default=384)
     ap.add_argument("--width", type=int, default=448)
