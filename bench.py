@@ -115,7 +115,7 @@ def parse_args(argv=None):
                     help="cpu = launcher rehearsal over gloo with a torch-CPU stand-in op")
     ap.add_argument("--fused-levels", default="0,1",
                     help="levels run as one fused warp->correlation launch (WarpCorrelation)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02g_l4corr_pmc.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02h_l4corr_pmc.json"),
                     help="committed PMC summary used when the live passes cannot run")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 PMC passes for roofline.traffic")
