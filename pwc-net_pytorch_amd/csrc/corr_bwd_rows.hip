@@ -315,9 +315,10 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   g.Wf = g.Wq4 + 8;
   g.S = g.Wq4 / 4;
   // the tallest band (least restaging of the R + 8 feature rows); channel slices fill the chip.
-  // CT 8 (channels per item and chunk) except on the dword path at 192 channels (l0: 4 gives
-  // the chunks for 4 slices, 10.7 against 11.5 us); profiles/r02e_corr_bwd_slices.txt
-  int R = 1, CT = (vec || C < 192) ? 8 : 4;
+  // CT (channels per item and chunk) 8 on the 16-B path; 2 on the dword path (l0 / l1: more,
+  // shorter chunks give more slices -- 10.6 -> 9.4 us at l0, 12.0 -> 11.6 at l1;
+  // profiles/r02e_corr_bwd_slices.txt)
+  int R = 1, CT = vec ? 8 : 2;
   for (int r : {3, 2, 1}) {
     if (9 * r * 2 * g.S > NT) continue;
     R = r;
@@ -389,6 +390,8 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   PWC_BWD(false, 8, 32)
   PWC_BWD(false, 4, 8)
   PWC_BWD(false, 4, 16)
+  PWC_BWD(false, 2, 4)
+  PWC_BWD(false, 2, 8)
 #undef PWC_BWD
   return hipErrorNotSupported;
 }
