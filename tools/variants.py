@@ -19,7 +19,8 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from kbench import timeit  # noqa: E402
 from pwcnet_amd import _lib  # noqa: E402
-from pwcnet_amd.ops import corr_forward, warp_forward, corr_backward, warp_backward  # noqa: E402
+from pwcnet_amd.ops import (corr_backward, corr_forward, warp_backward,  # noqa: E402
+                            warp_corr_forward, warp_forward)
 
 
 def main():
@@ -56,6 +57,8 @@ def main():
         "warp": (lambda s: warp_forward(s["x2"], s["fl"]), (2 * C * h * w + 2 * h * w) * B * esz),
         "corr_bwd": (lambda s: corr_backward(s["x1"], s["x2"], s["go"], 9, 1, 9, 1, 2),
                      (4 * C * h * w + 81 * h * w) * B * esz),
+        "warp_corr": (lambda s: warp_corr_forward(s["x1"], s["x2"], s["fl"], 9, 1, 9, 1, 2),
+                      (3 * C * h * w + 2 * h * w + 81 * h * w) * B * esz),
         "warp_bwd": (lambda s: warp_backward(s["x2"], s["fl"], s["gw"]),
                      (3 * C * h * w + 4 * h * w) * B * esz),
     }
