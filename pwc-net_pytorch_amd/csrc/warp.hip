@@ -618,6 +618,9 @@ hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int
   // measured best at one group of 4 (r02d_warp_cb_sweep)
   int cfg = warp_cfg();
   if (cfg == 0 && sizeof(T) == 2 && npix >= 16384) cfg = 9;
+  // fp32 on large grids: 8 channels per thread (config-2 l3 5.57 -> 5.32 us, l4 equal; l2
+  // stays at 4: 3.52 against 3.68 -- 300 launches each, profiles/r02e_warp_fp32_cfg.txt)
+  if (cfg == 0 && sizeof(T) == 4 && npix >= 16384) cfg = 5;
   switch (cfg) {
     case 1: PWC_WARP_LAUNCH(8, 1, false); break;
     case 2: PWC_WARP_LAUNCH(2, 1, false); break;
