@@ -115,6 +115,10 @@ def parse_args(argv=None):
                     help="cpu = launcher rehearsal over gloo with a torch-CPU stand-in op")
     ap.add_argument("--fused-levels", default="0,1",
                     help="levels run as one fused warp->correlation launch (WarpCorrelation)")
+    ap.add_argument("--group", default="on", choices=["on", "off"],
+                    help="issue the fused levels as one group (pwc_warp_corr_forward_group: "
+                         "the bench's levels take independent inputs, so l0 + l1 share one "
+                         "launch); off = one call per level")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02h_l4corr_pmc.json"),
                     help="committed PMC summary used when the live passes cannot run")
     ap.add_argument("--no-pmc", action="store_true",
@@ -192,13 +196,14 @@ class HipPass:
     P = (CORR_ARGS["pad_size"], CORR_ARGS["kernel_size"], CORR_ARGS["max_displacement"],
          CORR_ARGS["stride1"], CORR_ARGS["stride2"])
 
-    def __init__(self, dev, dtype, fused):
+    def __init__(self, dev, dtype, fused, group=False):
         from pwcnet_amd import _lib
         from pwcnet_amd.ops import corr_forward, warp_forward
         self._lib = _lib
         self.lib = _lib.load()  # raises if the HIP library is missing: there is no fallback
         self.warp_forward, self.corr_forward = warp_forward, corr_forward
         self.dev, self.dtype, self.fused = dev, dtype, fused
+        self.group = group
         self.dcode = _lib.DTYPE_CODES[dtype]
 
     def bind(self, s):
@@ -228,6 +233,7 @@ class HipPass:
         sp = self.sp
         c_int = ctypes.c_int
         calls = []
+        grouped = self.grouped_levels(s)
         for l, lv in enumerate(s):
             B, C, h, w = lv["x1"].shape
             dims = [c_int(B), c_int(C), c_int(h), c_int(w)]
@@ -237,7 +243,13 @@ class HipPass:
                                                    *dims, c_int(self.dcode), sp), f"warp l{l}"))
             if l == len(s) - 1:
                 continue
-            if l in self.fused:
+            if l in grouped:
+                if l == grouped[0]:
+                    arr = self.group_array(s, grouped)
+                    calls.append((L.pwc_warp_corr_forward_group,
+                                  (arr, c_int(len(grouped)), *cp, c_int(1), c_int(self.dcode),
+                                   sp), f"levels {grouped}"))
+            elif l in self.fused:
                 calls.append((L.pwc_warp_corr_forward,
                               (p(lv["x1"]), p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]),
                                p(lv["corr"]), *dims, *cp, c_int(1), c_int(self.dcode),
@@ -269,6 +281,29 @@ class HipPass:
         if ret != 1:
             self._lib.check(ret, "bench corr_l4")
 
+    def grouped_levels(self, s):
+        """The fused levels issued as one pwc_warp_corr_forward_group call (>= 2 of them)."""
+        lv = sorted(l for l in self.fused if l < len(s) - 1)
+        # the paired kernel is the fp32 band kernel; other dtypes keep per-level calls with
+        # their split-channel workspaces
+        ok = self.group and len(lv) >= 2 and self.dtype == torch.float32
+        return lv if ok else []
+
+    def group_array(self, s, levels):
+        """The problem list of one group call, kept alive on the buffer set."""
+        key = ("group", tuple(levels))
+        arr = s[0].get(key)
+        if arr is None:
+            T = self._lib.WarpCorrProblem
+            arr = (T * len(levels))()
+            for i, l in enumerate(levels):
+                lv = s[l]
+                B, C, h, w = lv["x1"].shape
+                arr[i] = T(lv["x1"].data_ptr(), lv["x2"].data_ptr(), lv["flow"].data_ptr(),
+                           lv["x2w"].data_ptr(), lv["corr"].data_ptr(), B, C, h, w)
+            s[0][key] = arr
+        return arr
+
     @staticmethod
     def _p(t):
         return ctypes.c_void_p(t.data_ptr())
@@ -277,9 +312,16 @@ class HipPass:
         """l0..l3 (warp + corr; fused levels as one WarpCorrelation launch that also emits
         x2_warp) and the l4 warp, all direct C-ABI calls on the bound buffers."""
         L, P, p = self.lib, self.P, self._p
+        grouped = self.grouped_levels(s)
         for l, lv in enumerate(s[:-1]):
             B, C, h, w = lv["x1"].shape
-            if l in self.fused:
+            if l in grouped:
+                ret = 1
+                if l == grouped[0]:
+                    ret = L.pwc_warp_corr_forward_group(self.group_array(s, grouped),
+                                                        len(grouped), *P, 1, self.dcode,
+                                                        self.sp)
+            elif l in self.fused:
                 ret = L.pwc_warp_corr_forward(p(lv["x1"]), p(lv["x2"]), p(lv["flow"]),
                                               p(lv["x2w"]), p(lv["corr"]), B, C, h, w, *P, 1,
                                               self.dcode, p(lv["ws"]), lv["nws"], self.sp)
@@ -627,7 +669,7 @@ def main(argv=None):
         sets = [checked_set(list(range(rank * B, rank * B + B)), shapes, dev, dtype)]
         nsets = 1
     else:
-        pass_ = HipPass(dev, dtype, fused)
+        pass_ = HipPass(dev, dtype, fused, group=args.group == "on")
         per_set = sum((2 * C * h * w + 2 * h * w + 81 * h * w + C * h * w) * B * esz
                       for C, h, w in shapes)
         nsets = args.sets or max(2, int(np.ceil(2 * 256 * 2 ** 20 / per_set)))
@@ -766,6 +808,7 @@ def main(argv=None):
             "parallelism": f"dp{world} (batch-sharded replicas, no data-path collective)",
             "buffer_sets": nsets,
             "fused_levels": sorted(fused),
+            "grouped_levels": (pass_.grouped_levels(shapes) if not cpu else []),
             "graph": bool(graphs),
             "timing": timing,
             "device": "cpu (launcher rehearsal: torch-CPU stand-in, not the product path)"

@@ -181,6 +181,26 @@ PWC_API int pwc_warp_corr_forward(const void* in1, const void* x2, const void* f
                           int kernel_size, int max_displacement, int stride1, int stride2,
                           int corr_multiply, int dtype, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* Several INDEPENDENT warp -> correlation problems (e.g. the pyramid levels of different
+ * batches in flight, or of the bench's synthetic levels; inside one forward of the model the
+ * levels depend on each other and are not a group).  Each problem is one pwc_warp_corr_forward
+ * call with x2_warp required (not NULL); problems of model.py:24's configuration in fp32 that
+ * take the fused band kernel are paired into ONE launch whose two grids share the CUs
+ * (the coarse levels' workgroups are latency-bound: 384x448 l0 + l1 run side by side), the
+ * rest run one pwc_warp_corr_forward call each, without a workspace.  Values are those of
+ * separate pwc_warp_corr_forward calls, bit for bit.  Returns 1 on success. */
+typedef struct {
+  const void* in1;
+  const void* x2;
+  const void* flow;
+  void* x2_warp;
+  void* out;
+  int B, C, H, W;
+} pwc_warp_corr_problem;
+PWC_API int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, int count,
+                                        int pad_size, int kernel_size, int max_displacement,
+                                        int stride1, int stride2, int corr_multiply, int dtype,
+                                        void* stream);
 #ifdef __cplusplus
 }
 #endif

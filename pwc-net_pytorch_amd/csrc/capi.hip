@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/pwc_hotpath.h"
 #include "pwc_common.cuh"
@@ -30,6 +31,8 @@ template <typename T>
 hipError_t upsample_warp_forward_t(const void*, const void*, void*, void*, int, int, int, int,
                                    hipStream_t);
 hipError_t flow_up2_backward_f32(const void*, void*, int, int, int, hipStream_t);
+hipError_t warp_corr_band_pair_f32(const BandProblem& a, const BandProblem& b, float divisor_a,
+                                   float divisor_b, hipStream_t stream);
 hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                               int, float, int, hipStream_t);
 }  // namespace pwc
@@ -583,6 +586,57 @@ int pwc_warp_corr_forward(const void* in1, const void* x2, const void* flow, voi
   return corr_forward_impl(fn, in1, warped, out, B, C, H, W, pad_size, kernel_size,
                            max_displacement, stride1, stride2, dtype, corr_ws, corr_ws_bytes,
                            stream);
+}
+
+int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, int count, int pad_size,
+                                int kernel_size, int max_displacement, int stride1, int stride2,
+                                int corr_multiply, int dtype, void* stream) {
+  const char* fn = "pwc_warp_corr_forward_group";
+  if (count < 0 || (count > 0 && !problems)) return fail(fn, "invalid problem list");
+  for (int i = 0; i < count; ++i) {
+    const pwc_warp_corr_problem& q = problems[i];
+    int OC, Ho, Wo;
+    if (!dims_ok(q.B, q.C, q.H, q.W)) return fail(fn, "negative dimension");
+    if (!corr_shape(q.H, q.W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC,
+                    &Ho, &Wo))
+      return fail(fn, "invalid correlation parameters");
+    if ((size_t)q.B * q.C * q.H * q.W && !q.x2_warp) return fail(fn, "x2_warp is required");
+  }
+  // fused pairs first (in list order), then every problem left, one call each
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<char> done((size_t)count, 0);
+  if (!fused_disabled() && warp_corr_fusable(pad_size, kernel_size, max_displacement, stride1,
+                                             stride2, dtype)) {
+    int open = -1;
+    for (int i = 0; i < count; ++i) {
+      const pwc_warp_corr_problem& q = problems[i];
+      if ((size_t)q.B * q.C * q.H * q.W == 0) continue;
+      if (open < 0) {
+        open = i;
+        continue;
+      }
+      const pwc_warp_corr_problem& p = problems[open];
+      const pwc::BandProblem a{p.in1, p.x2, p.flow, p.x2_warp, p.out, p.B, p.C, p.H, p.W};
+      const pwc::BandProblem b{q.in1, q.x2, q.flow, q.x2_warp, q.out, q.B, q.C, q.H, q.W};
+      const hipError_t e = pwc::warp_corr_band_pair_f32(a, b, (float)p.C, (float)q.C, s);
+      if (e == hipErrorNotSupported) {
+        open = i;  // no pair with the open one: try the next problem against this one
+        continue;
+      }
+      if (!check_launch(fn, e)) return 0;
+      done[(size_t)open] = done[(size_t)i] = 1;
+      open = -1;
+    }
+  }
+  for (int i = 0; i < count; ++i) {
+    if (done[(size_t)i]) continue;
+    const pwc_warp_corr_problem& q = problems[i];
+    if (!pwc_warp_corr_forward(q.in1, q.x2, q.flow, q.x2_warp, q.out, q.B, q.C, q.H, q.W,
+                               pad_size, kernel_size, max_displacement, stride1, stride2,
+                               corr_multiply, dtype, nullptr, 0, stream))
+      return 0;
+  }
+  return 1;
 }
 
 }  // extern "C"

@@ -129,6 +129,16 @@ __device__ __forceinline__ float epi_act(float v, float slope) { return v > 0.f 
 OutEpi current_epi();
 inline bool epi_is_default(const OutEpi& e) { return e.ostride == 0 && e.slope == 1.f; }
 
+// One warp -> correlation problem of a grouped launch (capi.hip's pwc_warp_corr_problem).
+struct BandProblem {
+  const void* f1;
+  const void* x2;
+  const void* flow;
+  void* x2w;
+  void* out;
+  int B, C, H, W;
+};
+
 // Debug / measurement knobs: ONE environment variable, PWC_DEBUG="name=value,name=value",
 // parsed once per process (capi.hip).  Unset knobs return `def`; production runs set nothing.
 // Kernels never read it -- launchers turn a knob into a template choice or an argument.

@@ -83,18 +83,39 @@ __device__ unsigned long long g_band_dbg[4096 * 8];
       g_band_dbg[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();             \
   } while (0)
 
-template <int R, int T, bool WARP>
-__global__ __launch_bounds__(NT, 1) void warp_corr_band(
-    const float* __restrict__ f1, const float* __restrict__ x2, const float* __restrict__ flow,
-    float* __restrict__ x2w, float* __restrict__ out, int C, int H, int W, float divisor,
-    float inv_divisor, float halfx, float halfy, Geo g, OutEpi epi) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+// One problem of a (possibly grouped) launch: the tensors and geometry of one level.
+struct Prob {
+  const float* f1;
+  const float* x2;
+  const float* flow;
+  float* x2w;
+  float* out;
+  int C, H, W;
+  float divisor, inv_divisor, halfx, halfy;
+  Geo g;
+};
+
+// The workgroup body; `bid` is the workgroup's index inside its problem's grid.  MJ: channels
+// per staging batch per thread (loads in flight; MAXJ for the single-level kernel, 16 under
+// the two-workgroups-per-CU register cap of the grouped kernel).
+template <int R, int T, bool WARP, int MJ>
+__device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds, const Prob& P,
+                                          const OutEpi& epi) {
+  const float* __restrict__ f1 = P.f1;
+  const float* __restrict__ x2 = P.x2;
+  const float* __restrict__ flow = P.flow;
+  float* __restrict__ x2w = P.x2w;
+  float* __restrict__ out = P.out;
+  const int C = P.C, H = P.H, W = P.W;
+  const float divisor = P.divisor, inv_divisor = P.inv_divisor, halfx = P.halfx,
+              halfy = P.halfy;
+  const Geo& g = P.g;
   constexpr int NR2 = R + T - 1;  // f2 parity rows staged
   BAND_MARK(0);
   const int t = threadIdx.x;
-  // blockIdx = tg * units + unit: the T-groups of one band are units apart (same XCD when
+  // bid = tg * units + unit: the T-groups of one band are units apart (same XCD when
   // units % 8 == 0), so they meet the same x1 / x2 rows in one L2 -- speed only
-  const int unit = blockIdx.x % g.units, tg = blockIdx.x / g.units;
+  const int unit = bid % g.units, tg = bid / g.units;
   const int b = unit % g.nb, np = unit / g.nb;
   const int p = np & 1, n = np >> 1;
   const int hp = (H - p + 1) >> 1;  // image rows of parity p
@@ -154,10 +175,10 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(
   // channels per thread (uniform): iterations past it are skipped by a scalar branch
   const int nj1 = (C + ncg1 - 1) / ncg1, nj2 = (C + ncg2 - 1) / ncg2;
   int jb1 = 0, jb2 = 0;  // channel slot of the batch's first j
-  float v1[MAXJ];
+  float v1[MJ];
   auto f1_issue = [&]() {
 #pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
+    for (int j = 0; j < MJ; ++j) {
       if (jb1 + j >= nj1) break;
       v1[j] = __uint_as_float(
           __builtin_amdgcn_raw_buffer_load_b32(rs1, (int)vo1, (int)((jb1 + j) * cs1), 0));
@@ -165,7 +186,7 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(
   };
   auto f1_store = [&]() {
 #pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
+    for (int j = 0; j < MJ; ++j) {
       if (jb1 + j >= nj1) break;
       const int c = cg1 + (jb1 + j) * ncg1;
       if (ok1 && c < C) f1s[c * ch1 + dst1] = v1[j];
@@ -195,10 +216,10 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(
   }
   const uint32_t voA = ok2 ? (cbase2 + (WARP ? kp.i0 : src2)) * 4u : kOOB;
   const uint32_t voB = ok2 ? (cbase2 + kp.i1) * 4u : kOOB;
-  float lo[MAXJ][2], hi[MAXJ][2];
+  float lo[MJ][2], hi[MJ][2];
   auto f2_issue = [&]() {
 #pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
+    for (int j = 0; j < MJ; ++j) {
       if (jb2 + j >= nj2) break;
       const int so = (int)((jb2 + j) * cs2);
       if constexpr (WARP) {
@@ -217,7 +238,7 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(
   // load was consumed (vmcnt retires in issue order: a store between loads delays them)
   auto f2_store = [&]() {
 #pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
+    for (int j = 0; j < MJ; ++j) {
       if (jb2 + j >= nj2) break;
       const int c = cg2 + (jb2 + j) * ncg2;
       float val;
@@ -241,7 +262,7 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(
     }
     if constexpr (WARP) {
 #pragma unroll
-      for (int j = 0; j < MAXJ; ++j) {
+      for (int j = 0; j < MJ; ++j) {
         if (jb2 + j >= nj2) break;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lo[j][0]), rsw, (int)vow,
                                               (int)((jb2 + j) * cs2), 2 /* nt */);
@@ -251,12 +272,12 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(
   f2_issue();
   f1_store();
   f2_store();
-  // further batches when a thread has more than MAXJ channels (uniform trip count)
-  const int nbat1 = (nj1 + MAXJ - 1) / MAXJ;
-  const int nbat2 = (nj2 + MAXJ - 1) / MAXJ;
+  // further batches when a thread has more than MJ channels (uniform trip count)
+  const int nbat1 = (nj1 + MJ - 1) / MJ;
+  const int nbat2 = (nj2 + MJ - 1) / MJ;
   for (int b = 1; b < max(nbat1, nbat2); ++b) {
-    jb1 = b * MAXJ;
-    jb2 = b * MAXJ;
+    jb1 = b * MJ;
+    jb2 = b * MJ;
     const bool m1 = b < nbat1, m2 = b < nbat2;
     if (m1) f1_issue();
     if (m2) f2_issue();
@@ -349,6 +370,27 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(
   }
 }
 
+template <int R, int T, bool WARP>
+__global__ __launch_bounds__(NT, 1) void warp_corr_band(Prob P, OutEpi epi) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  band_body<R, T, WARP, MAXJ>((int)blockIdx.x, lds, P, epi);
+}
+
+// Two independent problems in one launch (e.g. two coarse levels, or two requests): blocks
+// [0, nblk0) run problem 0's grid, the rest problem 1's.  Each workgroup of these latency-bound
+// grids holds its CU for a few microseconds at two waves per SIMD, so the two grids co-reside
+// (<= 128 VGPRs: two 512-thread workgroups per CU; the launcher checks that the two LDS
+// footprints fit one CU together) instead of running one after the other.
+template <int R0, int T0, int R1, int T1>
+__global__ __launch_bounds__(NT, 2) void warp_corr_band_pair(Prob P0, Prob P1, int nblk0,
+                                                             OutEpi epi) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if ((int)blockIdx.x < nblk0)
+    band_body<R0, T0, true, 16>((int)blockIdx.x, lds, P0, epi);
+  else
+    band_body<R1, T1, true, 16>((int)blockIdx.x - nblk0, lds, P1, epi);
+}
+
 struct Cfg {
   int R, T;
 };
@@ -365,9 +407,7 @@ static bool env_cfg(int* R, int* T, int* G) {
 }
 
 template <int R, int T, bool WARP>
-static hipError_t launch(const float* f1, const float* x2, const float* flow, float* x2w,
-                         float* out, int B, int C, int H, int W, float divisor, float inv,
-                         float halfx, float halfy, Geo g, size_t lds, hipStream_t stream) {
+static hipError_t launch(const Prob& P, size_t lds, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&warp_corr_band<R, T, WARP>),
@@ -378,9 +418,8 @@ static hipError_t launch(const float* f1, const float* x2, const float* flow, fl
   const int ntg = (D + T - 1) / T;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);
-  hipExtLaunchKernelGGL((warp_corr_band<R, T, WARP>), dim3((unsigned)(g.units * ntg)), dim3(NT),
-                        lds, stream, ev0, ev1, 0, f1, x2, flow, x2w, out, C, H, W, divisor, inv,
-                        halfx, halfy, g, current_epi());
+  hipExtLaunchKernelGGL((warp_corr_band<R, T, WARP>), dim3((unsigned)(P.g.units * ntg)),
+                        dim3(NT), lds, stream, ev0, ev1, 0, P, current_epi());
   return hipGetLastError();
 }
 
@@ -431,6 +470,51 @@ extern "C" __attribute__((visibility("default"))) int pwc_debug_band_reset(void)
   return hipMemcpyToSymbol(HIP_SYMBOL(band::g_band_dbg), zeros, sizeof(zeros)) == hipSuccess;
 }
 
+namespace band {
+
+// The per-level (R, T) choice (measured at 384x448, B = 8, tools/kbench.py), the geometry and
+// the kernel arguments of one problem; false when it does not take a band workgroup.
+static bool make_prob(const void* f1, const void* x2, const void* flow, void* x2w, void* out,
+                      int B, int C, int H, int W, float divisor, int warp, int* R, int* T,
+                      Prob* P, size_t* lds) {
+  if (W < 2 || (size_t)B * C * H * W >= (1ull << 31) || (size_t)B * 81 * H * W >= (1ull << 31))
+    return false;
+  // the whole parity half in one band where it fits, one tj per workgroup
+  int Greq = 0;
+  const int hp = (H + 1) / 2;
+  *T = 1;
+  if (!env_cfg(R, T, &Greq)) {
+    if (hp <= 3) {
+      *R = 3;  // l0: 7.7 us (warp 3.1 + correlation 10.9 unfused)
+      *T = 1;
+    } else if (hp <= 6) {
+      *R = 2;  // l1: fused 10.7 us (3.4 + 13.4 unfused); plain correlation 7.8 us with T = 1
+      *T = warp ? 3 : 1;
+    } else {
+      *R = 3;  // l2 and larger (the bench keeps l2..l4 unfused: 17.7 vs 3.6 + 11.4 us at l2)
+      *T = 3;
+    }
+  }
+  if (!make_geo(B, C, H, W, *R, *T, Greq, &P->g, lds)) return false;
+  P->f1 = (const float*)f1;
+  P->x2 = (const float*)x2;
+  P->flow = (const float*)flow;
+  P->x2w = (float*)x2w;
+  P->out = (float*)out;
+  P->C = C;
+  P->H = H;
+  P->W = W;
+  P->halfx = (float)((W - 1.0) / 2.0);
+  P->halfy = (float)((H - 1.0) / 2.0);
+  int ex;
+  const float m = std::frexp(divisor, &ex);
+  P->divisor = divisor;
+  P->inv_divisor = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
+  return true;
+}
+
+}  // namespace band
+
 // Fused warp -> correlation for Correlation(pad == md in {8, 9}, k 1, s1 1, s2 2), fp32,
 // raster channel order.  hipErrorNotSupported when the level does not fit a band workgroup
 // (the caller then runs the warp and correlation kernels separately).  `warp` = 0 correlates
@@ -442,39 +526,14 @@ hipError_t warp_corr_band_f32(const void* f1, const void* x2, const void* flow, 
   if (B == 0 || C == 0 || H == 0 || W == 0) return hipSuccess;
   if (W < 2 || (size_t)B * C * H * W >= (1ull << 31) || (size_t)B * 81 * H * W >= (1ull << 31))
     return hipErrorNotSupported;
-  // per-level choice: the whole parity half in one band where it fits, one tj per workgroup
-  int R = 0, T = 1, Greq = 0;
-  const int hp = (H + 1) / 2;
-  if (!env_cfg(&R, &T, &Greq)) {  // measured at 384x448, B = 8 (tools/kbench.py)
-    if (hp <= 3) {
-      R = 3;  // l0: 7.7 us (warp 3.1 + correlation 10.9 unfused)
-      T = 1;
-    } else if (hp <= 6) {
-      R = 2;  // l1: fused 10.7 us (3.4 + 13.4 unfused); plain correlation 7.8 us with T = 1
-      T = warp ? 3 : 1;
-    } else {
-      R = 3;  // l2 and larger (the bench keeps l2..l4 unfused: 17.7 vs 3.6 + 11.4 us at l2)
-      T = 3;
-    }
-  }
-  Geo g;
+  int R = 0, T = 1;
+  Prob P;
   size_t lds;
-  if (!make_geo(B, C, H, W, R, T, Greq, &g, &lds)) return hipErrorNotSupported;
-  const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
-  int ex;
-  const float m = std::frexp(divisor, &ex);
-  const float inv = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
-  const float* a = (const float*)f1;
-  const float* b = (const float*)x2;
-  const float* fl = (const float*)flow;
-  float* w = (float*)x2w;
-  float* o = (float*)out;
+  if (!make_prob(f1, x2, flow, x2w, out, B, C, H, W, divisor, warp, &R, &T, &P, &lds))
+    return hipErrorNotSupported;
 #define PWC_BAND(RR, TT)                                                                     \
   if (R == RR && T == TT)                                                                    \
-    return warp ? launch<RR, TT, true>(a, b, fl, w, o, B, C, H, W, divisor, inv, halfx, halfy, \
-                                       g, lds, stream)                                       \
-                : launch<RR, TT, false>(a, b, fl, w, o, B, C, H, W, divisor, inv, halfx,       \
-                                        halfy, g, lds, stream);
+    return warp ? launch<RR, TT, true>(P, lds, stream) : launch<RR, TT, false>(P, lds, stream);
   PWC_BAND(3, 1)
   PWC_BAND(6, 1)
   PWC_BAND(4, 1)
@@ -484,6 +543,52 @@ hipError_t warp_corr_band_f32(const void* f1, const void* x2, const void* flow, 
   PWC_BAND(3, 3)
   PWC_BAND(6, 3)
 #undef PWC_BAND
+  return hipErrorNotSupported;
+}
+
+// Two fused warp -> correlation problems (warp = 1, fp32, raster) in ONE launch
+// (warp_corr_band_pair); hipErrorNotSupported when either does not take a band workgroup, their
+// (R, T) pair has no instantiation, or their LDS footprints do not fit one CU together -- the
+// caller then launches them one after the other.
+hipError_t warp_corr_band_pair_f32(const BandProblem& a, const BandProblem& b, float divisor_a,
+                                   float divisor_b, hipStream_t stream) {
+  using namespace band;
+  if (debug_knob("band_pair", 1) == 0 || !epi_is_default(current_epi()))
+    return hipErrorNotSupported;
+  for (const BandProblem* q : {&a, &b})
+    if (q->B == 0 || q->C == 0 || q->H == 0 || q->W == 0) return hipErrorNotSupported;
+  int R0 = 0, T0 = 1, R1 = 0, T1 = 1;
+  Prob P0, P1;
+  size_t l0, l1;
+  if (!make_prob(a.f1, a.x2, a.flow, a.x2w, a.out, a.B, a.C, a.H, a.W, divisor_a, 1, &R0, &T0,
+                 &P0, &l0) ||
+      !make_prob(b.f1, b.x2, b.flow, b.x2w, b.out, b.B, b.C, b.H, b.W, divisor_b, 1, &R1, &T1,
+                 &P1, &l1))
+    return hipErrorNotSupported;
+  // the kernel allocates max(l0, l1) to every workgroup: two of them must fit one CU
+  const size_t lds = l0 > l1 ? l0 : l1;
+  if (2 * lds > 160 * 1024) return hipErrorNotSupported;
+  const int n0 = P0.g.units * ((D + T0 - 1) / T0);
+  const int n1 = P1.g.units * ((D + T1 - 1) / T1);
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+#define PWC_PAIR(A0, B0, A1, B1)                                                              \
+  if (R0 == A0 && T0 == B0 && R1 == A1 && T1 == B1) {                                         \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      hipError_t e = hipFuncSetAttribute(                                                     \
+          reinterpret_cast<const void*>(&warp_corr_band_pair<A0, B0, A1, B1>),                \
+          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+      if (e != hipSuccess) return e;                                                          \
+      attr = true;                                                                            \
+    }                                                                                         \
+    take_launch_events(&ev0, &ev1);                                                           \
+    hipExtLaunchKernelGGL((warp_corr_band_pair<A0, B0, A1, B1>), dim3((unsigned)(n0 + n1)),   \
+                          dim3(NT), lds, stream, ev0, ev1, 0, P0, P1, n0, current_epi());     \
+    return hipGetLastError();                                                                 \
+  }
+  PWC_PAIR(3, 1, 2, 3)  // PWC-Net l0 + l1 (384 x 448: 6 x 7 and 12 x 14)
+  PWC_PAIR(2, 3, 3, 1)
+#undef PWC_PAIR
   return hipErrorNotSupported;
 }
 

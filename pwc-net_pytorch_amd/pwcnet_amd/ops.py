@@ -404,6 +404,51 @@ def warp_corr_forward(input1, x2, flow, pad_size, kernel_size, max_displacement,
     return out, x2w
 
 
+def warp_corr_forward_group(problems, pad_size, kernel_size, max_displacement, stride1,
+                            stride2, corr_multiply=1):
+    """[(corr, x2_warp)] for a list of INDEPENDENT (input1, x2, flow) problems -- one
+    ``warp_corr_forward`` each, bit for bit, but problems that take the fused band kernel are
+    paired into one launch whose two grids share the CUs (pwc_warp_corr_forward_group).  Inside
+    one model forward the pyramid levels depend on each other and are not a group."""
+    if not problems:
+        return []
+    items, outs = [], []
+    dt = None
+    for (input1, x2, flow) in problems:
+        _check_inputs("WarpCorrelation", input1, x2, flow)
+        if input1.shape != x2.shape:
+            raise ValueError(f"WarpCorrelation: input shapes differ {tuple(input1.shape)} vs "
+                             f"{tuple(x2.shape)}")
+        B, C, H, W = input1.shape
+        if tuple(flow.shape) != (B, 2, H, W):
+            raise ValueError(f"WarpCorrelation: flow shape {tuple(flow.shape)} != "
+                             f"{(B, 2, H, W)}")
+        if input1.device != problems[0][0].device:
+            raise ValueError("WarpCorrelation group: problems on different devices")
+        code = _lib.DTYPE_CODES[input1.dtype]
+        if dt is not None and code != dt:
+            raise ValueError("WarpCorrelation group: problems of different dtypes")
+        dt = code
+        _i32(B, C, H, W, input1.numel())
+        input1, x2, flow = input1.contiguous(), x2.contiguous(), flow.contiguous()
+        OC, Ho, Wo = _lib.corr_output_shape(H, W, pad_size, kernel_size, max_displacement,
+                                            stride1, stride2)
+        out = torch.empty((B, OC, Ho, Wo), dtype=input1.dtype, device=input1.device)
+        x2w = torch.empty_like(x2)
+        items.append((input1, x2, flow, x2w, out))
+        outs.append((out, x2w))
+    arr = (_lib.WarpCorrProblem * len(items))()
+    for i, (a, b, f, w, o) in enumerate(items):
+        B, C, H, W = a.shape
+        arr[i] = _lib.WarpCorrProblem(a.data_ptr(), b.data_ptr(), f.data_ptr(), w.data_ptr(),
+                                      o.data_ptr(), B, C, H, W)
+    dev = items[0][0].device
+    _lib.check(_lib.load().pwc_warp_corr_forward_group(
+        arr, len(items), pad_size, kernel_size, max_displacement, stride1, stride2,
+        corr_multiply, dt, _stream(dev)), "WarpCorrelation_forward_group")
+    return outs
+
+
 class WarpCorrelationFunction(Function):
     """autograd for model.py:80-83 as one op: outputs (corr, x2_warp).  Backward chains the
     reference's two backward passes: correlation (cu:108-290) into the warped features, plus

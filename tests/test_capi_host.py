@@ -128,3 +128,25 @@ def test_cvl_channel_formula_matches_reference_order():
         dys, dxs = O.cvl_offsets(sr)
         for k, (dy, dx) in enumerate(zip(dys, dxs)):
             assert cvl_channel(dy, dx, sr) == k, (sr, dy, dx, k)
+
+
+def test_group_entry_host_checks():
+    """pwc_warp_corr_forward_group rejects a bad list before any launch: negative count,
+    a NULL list, a problem without x2_warp, invalid correlation parameters."""
+    from pwcnet_amd import _lib
+    lib = _lib.load()
+    P = _lib.WarpCorrProblem
+    assert lib.pwc_warp_corr_forward_group(None, -1, 9, 1, 9, 1, 2, 1, 0, None) == 0
+    assert b"invalid problem list" in lib.pwc_last_error()
+    assert lib.pwc_warp_corr_forward_group(None, 1, 9, 1, 9, 1, 2, 1, 0, None) == 0
+    arr = (P * 1)(P(1, 1, 1, None, 1, 1, 4, 6, 7))
+    assert lib.pwc_warp_corr_forward_group(arr, 1, 9, 1, 9, 1, 2, 1, 0, None) == 0
+    assert b"x2_warp is required" in lib.pwc_last_error()
+    arr = (P * 1)(P(1, 1, 1, 1, 1, -1, 4, 6, 7))
+    assert lib.pwc_warp_corr_forward_group(arr, 1, 9, 1, 9, 1, 2, 1, 0, None) == 0
+    assert b"negative dimension" in lib.pwc_last_error()
+    arr = (P * 1)(P(1, 1, 1, 1, 1, 1, 4, 6, 7))
+    assert lib.pwc_warp_corr_forward_group(arr, 1, 9, 1, 9, 1, 0, 1, 0, None) == 0
+    assert b"invalid correlation parameters" in lib.pwc_last_error()
+    # an empty list is a no-op
+    assert lib.pwc_warp_corr_forward_group(None, 0, 9, 1, 9, 1, 2, 1, 0, None) == 1

@@ -184,3 +184,47 @@ def test_warp_correlation_module_autograd():
     np.testing.assert_allclose(_np(x1.grad), g1, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(_np(x2.grad), gx2, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(_np(fl.grad), gfl, rtol=1e-4, atol=1e-4)  # config 5
+
+
+# grouped launches: lists of independent problems (pwc_warp_corr_forward_group)
+GROUPS = [
+    [(8, 192, 6, 7), (8, 128, 12, 14)],                  # the bench's l0 + l1: one paired launch
+    [(8, 128, 12, 14), (8, 192, 6, 7)],                  # the other order
+    [(2, 192, 6, 7), (3, 128, 12, 14), (2, 96, 24, 28)],  # a pair + an unfused level
+    [(1, 24, 13, 15), (2, 16, 7, 9), (0, 8, 6, 7), (1, 40, 11, 30)],  # ragged, an empty batch
+    [(2, 192, 6, 7)],                                   # a single problem
+]
+
+
+@pytest.mark.parametrize("group", GROUPS, ids=lambda g: "+".join("B{}C{}_{}x{}".format(*s)
+                                                                 for s in g))
+def test_fused_group_matches_single_calls(group):
+    """Each problem of a group equals its own warp_corr_forward call bit for bit (the paired
+    kernel runs the same workgroup body), and the oracle within the north-star tolerance."""
+    from pwcnet_amd.ops import warp_corr_forward, warp_corr_forward_group
+    data = [_inputs(_seed("group", i, s), *s) for i, s in enumerate(group)]
+    probs = [(_t(a), _t(b), _t(f)) for (a, b, f) in data]
+    outs = warp_corr_forward_group(probs, 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    assert len(outs) == len(group)
+    for (a, b, f), (x1, x2, fl), (out, x2w) in zip(data, probs, outs):
+        ref_o, ref_w = warp_corr_forward(x1, x2, fl, 9, 1, 9, 1, 2)
+        assert torch.equal(out, ref_o) and torch.equal(x2w, ref_w)
+        if a.shape[0] > 0 and a.shape[1] * a.shape[2] * a.shape[3] <= 192 * 12 * 14:
+            _check(a, b, f, out, x2w)
+
+
+def test_fused_group_pair_disabled_is_identical():
+    """The pair kernel against the one-launch-per-problem path of the same entry point."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import warp_corr_forward_group
+    data = [_inputs(21 + i, *s) for i, s in enumerate(GROUPS[0])]
+    probs = [(_t(a), _t(b), _t(f)) for (a, b, f) in data]
+    o1 = warp_corr_forward_group(probs, 9, 1, 9, 1, 2)
+    _lib.set_debug("band_pair=0")
+    try:
+        o2 = warp_corr_forward_group(probs, 9, 1, 9, 1, 2)
+    finally:
+        _lib.set_debug("")
+    for (p, q), (r, s) in zip(o1, o2):
+        assert torch.equal(p, r) and torch.equal(q, s)
