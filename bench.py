@@ -119,6 +119,10 @@ def parse_args(argv=None):
                     help="issue the fused levels as one group (pwc_warp_corr_forward_group: "
                          "the bench's levels take independent inputs, so l0 + l1 share one "
                          "launch); off = one call per level")
+    ap.add_argument("--warp-group", default="on", choices=["on", "off"],
+                    help="the unfused levels' warps (l2, l3, l4) as one pwc_warp_forward_group "
+                         "launch ahead of their correlations (independent inputs); off = one "
+                         "warp call per level")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02h_l4corr_pmc.json"),
                     help="committed PMC summary used when the live passes cannot run")
     ap.add_argument("--no-pmc", action="store_true",
@@ -196,7 +200,7 @@ class HipPass:
     P = (CORR_ARGS["pad_size"], CORR_ARGS["kernel_size"], CORR_ARGS["max_displacement"],
          CORR_ARGS["stride1"], CORR_ARGS["stride2"])
 
-    def __init__(self, dev, dtype, fused, group=False):
+    def __init__(self, dev, dtype, fused, group=False, warp_group=False):
         from pwcnet_amd import _lib
         from pwcnet_amd.ops import corr_forward, warp_forward
         self._lib = _lib
@@ -204,6 +208,7 @@ class HipPass:
         self.warp_forward, self.corr_forward = warp_forward, corr_forward
         self.dev, self.dtype, self.fused = dev, dtype, fused
         self.group = group
+        self.warp_group = warp_group
         self.dcode = _lib.DTYPE_CODES[dtype]
 
     def bind(self, s):
@@ -234,11 +239,16 @@ class HipPass:
         c_int = ctypes.c_int
         calls = []
         grouped = self.grouped_levels(s)
+        wg = self.warp_levels(s)
         for l, lv in enumerate(s):
             B, C, h, w = lv["x1"].shape
             dims = [c_int(B), c_int(C), c_int(h), c_int(w)]
             cp = [c_int(v) for v in P]
-            if l == len(s) - 1 or l not in self.fused:
+            if wg and l == wg[0]:
+                calls.append((L.pwc_warp_forward_group,
+                              (self.warp_array(s, wg), c_int(len(wg)), c_int(self.dcode), sp),
+                              f"warps {wg}"))
+            if (l == len(s) - 1 or l not in self.fused) and l not in wg:
                 calls.append((L.pwc_warp_forward, (p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]),
                                                    *dims, c_int(self.dcode), sp), f"warp l{l}"))
             if l == len(s) - 1:
@@ -289,6 +299,25 @@ class HipPass:
         ok = self.group and len(lv) >= 2 and self.dtype == torch.float32
         return lv if ok else []
 
+    def warp_levels(self, s):
+        """The unfused levels whose warps run as one pwc_warp_forward_group call."""
+        lv = [l for l in range(len(s)) if l == len(s) - 1 or l not in self.fused]
+        return lv if self.warp_group and len(lv) >= 2 else []
+
+    def warp_array(self, s, levels):
+        key = ("warps", tuple(levels))
+        arr = s[0].get(key)
+        if arr is None:
+            T = self._lib.WarpProblem
+            arr = (T * len(levels))()
+            for i, l in enumerate(levels):
+                lv = s[l]
+                B, C, h, w = lv["x2"].shape
+                arr[i] = T(lv["x2"].data_ptr(), lv["flow"].data_ptr(), lv["x2w"].data_ptr(),
+                           B, C, h, w)
+            s[0][key] = arr
+        return arr
+
     def group_array(self, s, levels):
         """The problem list of one group call, kept alive on the buffer set."""
         key = ("group", tuple(levels))
@@ -313,8 +342,14 @@ class HipPass:
         x2_warp) and the l4 warp, all direct C-ABI calls on the bound buffers."""
         L, P, p = self.lib, self.P, self._p
         grouped = self.grouped_levels(s)
+        wg = self.warp_levels(s)
         for l, lv in enumerate(s[:-1]):
             B, C, h, w = lv["x1"].shape
+            if wg and l == wg[0]:
+                ret = L.pwc_warp_forward_group(self.warp_array(s, wg), len(wg), self.dcode,
+                                               self.sp)
+                if ret != 1:
+                    self._lib.check(ret, f"bench warps {wg}")
             if l in grouped:
                 ret = 1
                 if l == grouped[0]:
@@ -326,8 +361,10 @@ class HipPass:
                                               p(lv["x2w"]), p(lv["corr"]), B, C, h, w, *P, 1,
                                               self.dcode, p(lv["ws"]), lv["nws"], self.sp)
             else:
-                ret = L.pwc_warp_forward(p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]), B, C, h, w,
-                                         self.dcode, self.sp)
+                ret = 1
+                if l not in wg:
+                    ret = L.pwc_warp_forward(p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]), B, C, h,
+                                             w, self.dcode, self.sp)
                 if ret == 1:
                     ret = L.pwc_corr_forward_ws(p(lv["x1"]), p(lv["x2w"]), p(lv["corr"]), B, C,
                                                 h, w, *P, 1, self.dcode, p(lv["ws"]), lv["nws"],
@@ -336,10 +373,11 @@ class HipPass:
                 self._lib.check(ret, f"bench level {l}")
         lv = s[-1]
         B, C, h, w = lv["x1"].shape
-        ret = L.pwc_warp_forward(p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]), B, C, h, w,
-                                 self.dcode, self.sp)
-        if ret != 1:
-            self._lib.check(ret, "bench l4 warp")
+        if len(s) - 1 not in wg:
+            ret = L.pwc_warp_forward(p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]), B, C, h, w,
+                                     self.dcode, self.sp)
+            if ret != 1:
+                self._lib.check(ret, "bench l4 warp")
 
     def corr_l4(self, s, events=None):
         """The l4 correlation; ``events`` (eager timing only) arms hipExtLaunchKernel's
@@ -669,7 +707,8 @@ def main(argv=None):
         sets = [checked_set(list(range(rank * B, rank * B + B)), shapes, dev, dtype)]
         nsets = 1
     else:
-        pass_ = HipPass(dev, dtype, fused, group=args.group == "on")
+        pass_ = HipPass(dev, dtype, fused, group=args.group == "on",
+                        warp_group=args.warp_group == "on")
         per_set = sum((2 * C * h * w + 2 * h * w + 81 * h * w + C * h * w) * B * esz
                       for C, h, w in shapes)
         nsets = args.sets or max(2, int(np.ceil(2 * 256 * 2 ** 20 / per_set)))
@@ -809,6 +848,7 @@ def main(argv=None):
             "buffer_sets": nsets,
             "fused_levels": sorted(fused),
             "grouped_levels": (pass_.grouped_levels(shapes) if not cpu else []),
+            "warp_grouped_levels": (pass_.warp_levels(shapes) if not cpu else []),
             "graph": bool(graphs),
             "timing": timing,
             "device": "cpu (launcher rehearsal: torch-CPU stand-in, not the product path)"

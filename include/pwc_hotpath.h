@@ -58,7 +58,7 @@ extern "C" {
 
 /* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
  * 4: fused warp -> correlation, 5: fused flow upsample -> warp, corr into a slice,
- * 6: pwc_set_debug). */
+ * 6: pwc_set_debug, 7: grouped warp / warp -> correlation launches). */
 PWC_API int pwc_abi_version(void);
 
 /* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
@@ -144,6 +144,21 @@ PWC_API int pwc_cost_volume_backward(const void* src, const void* tgt, const voi
  * flow is [B][2][H][W], channel 0 = u (horizontal), 1 = v (vertical), in pixels. */
 PWC_API int pwc_warp_forward(const void* x, const void* flow, void* out, int B, int C, int H, int W,
                      int dtype, void* stream);
+/* Several INDEPENDENT warps (e.g. the bench's synthetic pyramid levels, or the levels of
+ * different batches in flight; inside one model forward each level's warp needs the previous
+ * level's flow, so those are not a group) in one launch per 4 problems: the problems' grids are
+ * laid end to end in one flat grid, so they share one launch gap and fill each other's tails.
+ * Each problem's output equals a pwc_warp_forward call on it, bit for bit (same fmaf chain per
+ * element; only the channels-per-thread grouping follows the largest problem).  Replaces a
+ * sequence of WarpingLayer calls (modules.py:31-42); returns 1 on success. */
+typedef struct {
+  const void* x;
+  const void* flow;
+  void* out;
+  int B, C, H, W;
+} pwc_warp_problem;
+PWC_API int pwc_warp_forward_group(const pwc_warp_problem* problems, int count, int dtype,
+                                   void* stream);
 /* Adjoint of pwc_warp_forward (ATen grid_sampler_2d_backward with the reference's grid chain).
  * grad_x: every element is written once (no memset, no atomics): per 8x32 tile of grad_x the
  * output pixels whose bilinear corners land in the tile are gathered in fixed order (a

@@ -25,6 +25,8 @@ hipError_t corr_backward_t(const void*, const void*, const void*, void*, void*, 
                            int);
 template <typename T>
 hipError_t warp_forward_t(const void*, const void*, void*, int, int, int, int, hipStream_t);
+template <typename T>
+hipError_t warp_forward_group_t(const WarpProblem*, int, hipStream_t);
 hipError_t warp_backward_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                              int, hipStream_t);
 template <typename T>
@@ -140,7 +142,7 @@ int force_generic() { return pwc::debug_knob("corr_path", 0); }
 
 extern "C" {
 
-int pwc_abi_version(void) { return 6; }
+int pwc_abi_version(void) { return 7; }
 
 int pwc_set_debug(const char* spec) {
   pwc::debug_spec() = spec ? spec : "";
@@ -460,6 +462,36 @@ int pwc_warp_forward(const void* x, const void* flow, void* out, int B, int C, i
       break;
     case PWC_DTYPE_BF16:
       e = pwc::warp_forward_t<__hip_bfloat16>(x, flow, out, B, C, H, W, s);
+      break;
+    default:
+      return fail(fn, "unsupported dtype");
+  }
+  return check_launch(fn, e);
+}
+
+int pwc_warp_forward_group(const pwc_warp_problem* problems, int count, int dtype,
+                           void* stream) {
+  const char* fn = "pwc_warp_forward_group";
+  if (count < 0 || (count > 0 && !problems)) return fail(fn, "invalid problem list");
+  static_assert(sizeof(pwc_warp_problem) == sizeof(pwc::WarpProblem), "problem layout");
+  for (int i = 0; i < count; ++i) {
+    const pwc_warp_problem& q = problems[i];
+    if (!dims_ok(q.B, q.C, q.H, q.W)) return fail(fn, "negative dimension");
+    if ((size_t)q.B * q.C * q.H * q.W && (!q.x || !q.flow || !q.out))
+      return fail(fn, "null buffer");
+  }
+  const pwc::WarpProblem* p = reinterpret_cast<const pwc::WarpProblem*>(problems);
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case PWC_DTYPE_F32:
+      e = pwc::warp_forward_group_t<float>(p, count, s);
+      break;
+    case PWC_DTYPE_F16:
+      e = pwc::warp_forward_group_t<__half>(p, count, s);
+      break;
+    case PWC_DTYPE_BF16:
+      e = pwc::warp_forward_group_t<__hip_bfloat16>(p, count, s);
       break;
     default:
       return fail(fn, "unsupported dtype");

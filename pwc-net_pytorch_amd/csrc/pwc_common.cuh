@@ -139,6 +139,14 @@ struct BandProblem {
   int B, C, H, W;
 };
 
+// One warp problem of a grouped launch (capi.hip's pwc_warp_problem).
+struct WarpProblem {
+  const void* x;
+  const void* flow;
+  void* out;
+  int B, C, H, W;
+};
+
 // Debug / measurement knobs: ONE environment variable, PWC_DEBUG="name=value,name=value",
 // parsed once per process (capi.hip).  Unset knobs return `def`; production runs set nothing.
 // Kernels never read it -- launchers turn a knob into a template choice or an argument.

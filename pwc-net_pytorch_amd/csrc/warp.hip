@@ -98,15 +98,15 @@ __device__ __forceinline__ float up2_value(const T* __restrict__ f, const UpTap&
 // UP: `flow` is the coarse [B][2][H/2][W/2] flow of the previous level, upsampled in registers
 // (model.py:78); the channel-slice-0 threads also write the upsampled flow to `flow_up` when
 // it is not null (model.py:89/91 concatenates it).
-template <typename T, int CB, int NG, bool XCD, bool UP = false>
-__global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
-                                                       const T* __restrict__ flow,
-                                                       T* __restrict__ out, int B, int C, int H,
-                                                       int W, float halfx, float halfy,
-                                                       T* __restrict__ flow_up = nullptr) {
+// The body of one (pixel block bx, channel slice cy) of warp_fwd_kernel; the grouped launch
+// (warp_fwd_group) runs it on each problem's own block range.
+template <typename T, int CB, int NG, bool UP>
+__device__ __forceinline__ void warp_fwd_block(const T* __restrict__ x,
+                                               const T* __restrict__ flow, T* __restrict__ out,
+                                               int B, int C, int H, int W, float halfx,
+                                               float halfy, T* __restrict__ flow_up,
+                                               unsigned bx, unsigned cy) {
   const unsigned plane = (unsigned)(H * W);
-  // XCD: consecutive pixel blocks (which gather overlapping source rows) share an L2
-  const unsigned bx = XCD ? (unsigned)xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const unsigned idx = bx * 256u + threadIdx.x;
   if (idx >= (unsigned)B * plane) return;
   const unsigned n = idx / plane;
@@ -121,13 +121,13 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
     u = up2_value(flow + (2 * n + 0) * cplane, tp);
     v = up2_value(flow + (2 * n + 1) * cplane, tp);
     if constexpr (sizeof(T) == 4) {  // round like a stored fp32 flow, then use it
-      if (flow_up != nullptr && blockIdx.y == 0) {
+      if (flow_up != nullptr && cy == 0) {
         flow_up[(2 * n + 0) * plane + pix] = u;
         flow_up[(2 * n + 1) * plane + pix] = v;
       }
     } else {  // storage rounding first: the reference warps with the stored upsampled flow
       const T ut = from_f32<T>(u), vt = from_f32<T>(v);
-      if (flow_up != nullptr && blockIdx.y == 0) {
+      if (flow_up != nullptr && cy == 0) {
         flow_up[(2 * n + 0) * plane + pix] = ut;
         flow_up[(2 * n + 1) * plane + pix] = vt;
       }
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
   const Pairs kp = pairs(b, H, W);
   const Corners kc = corners(b, H, W);
   const float m00 = kc.m00, m01 = kc.m01, m10 = kc.m10, m11 = kc.m11;
-  const int cs = blockIdx.y * CB * NG;
+  const int cs = (int)cy * CB * NG;
   WarpGroup<T, CB> g[2];
   warp_load(g[0], x, n, C, plane, cs, W, kp, kc);
 #pragma unroll
@@ -170,6 +170,58 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
       }
     }
   }
+}
+
+template <typename T, int CB, int NG, bool XCD, bool UP = false>
+__global__ __launch_bounds__(256) void warp_fwd_kernel(const T* __restrict__ x,
+                                                       const T* __restrict__ flow,
+                                                       T* __restrict__ out, int B, int C, int H,
+                                                       int W, float halfx, float halfy,
+                                                       T* __restrict__ flow_up = nullptr) {
+  // XCD: consecutive pixel blocks (which gather overlapping source rows) share an L2
+  const unsigned bx = XCD ? (unsigned)xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  warp_fwd_block<T, CB, NG, UP>(x, flow, out, B, C, H, W, halfx, halfy, flow_up, bx,
+                                blockIdx.y);
+}
+
+// Up to kWarpGroupMax independent warps in ONE launch (pwc_warp_forward_group): problem i owns
+// the flat blocks [start[i], start[i+1]), laid out as its (channel slice, pixel block) grid, so
+// a launch gap and each small grid's tail are shared.  The XCD remap runs over the flat grid:
+// consecutive pixel blocks of one problem still share an L2.
+constexpr int kWarpGroupMax = 4;
+template <typename T>
+struct WarpGroupArgs {
+  const T* x[kWarpGroupMax];
+  const T* flow[kWarpGroupMax];
+  T* out[kWarpGroupMax];
+  int B[kWarpGroupMax], C[kWarpGroupMax], H[kWarpGroupMax], W[kWarpGroupMax];
+  float halfx[kWarpGroupMax], halfy[kWarpGroupMax];
+  unsigned gx[kWarpGroupMax];
+  unsigned start[kWarpGroupMax + 1];
+  int n;
+};
+
+template <typename T, int CB, int NG>
+__global__ __launch_bounds__(256) void warp_fwd_group(WarpGroupArgs<T> a) {
+  const unsigned g = (unsigned)xcd_remap(blockIdx.x, gridDim.x);
+  // scalar selects (uniform per workgroup), no dynamic indexing of the argument struct
+  const T *x = a.x[0], *flow = a.flow[0];
+  T* out = a.out[0];
+  int B = a.B[0], C = a.C[0], H = a.H[0], W = a.W[0];
+  float hx = a.halfx[0], hy = a.halfy[0];
+  unsigned gx = a.gx[0], s0 = 0;
+#pragma unroll
+  for (int i = 1; i < kWarpGroupMax; ++i) {
+    if (i < a.n && g >= a.start[i]) {
+      x = a.x[i], flow = a.flow[i], out = a.out[i];
+      B = a.B[i], C = a.C[i], H = a.H[i], W = a.W[i];
+      hx = a.halfx[i], hy = a.halfy[i], gx = a.gx[i], s0 = a.start[i];
+    }
+  }
+  const unsigned local = g - s0;
+  const unsigned cy = local / gx;
+  warp_fwd_block<T, CB, NG, false>(x, flow, out, B, C, H, W, hx, hy, nullptr, local - cy * gx,
+                                   cy);
 }
 
 // fp32 only: grad_x accumulated with atomics (zeroed by the launcher), grad_flow per pixel.
@@ -636,6 +688,62 @@ hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int
 #undef PWC_WARP_LAUNCH
   return hipGetLastError();
 }
+
+// Independent warps in one launch, kWarpGroupMax problems per launch (pwc_warp_forward_group).
+// The channels-per-thread choice follows the largest problem (warp_forward_t's large-grid
+// choice); each output element is the same fmaf chain as a separate call, bit for bit.
+template <typename T>
+hipError_t warp_forward_group_t(const WarpProblem* probs, int count, hipStream_t stream) {
+  for (int i0 = 0; i0 < count; i0 += kWarpGroupMax) {
+    WarpGroupArgs<T> a{};
+    size_t big = 0;
+    int n = 0;
+    unsigned total = 0;
+    bool cb8 = false;
+    for (int i = i0; i < count && i < i0 + kWarpGroupMax; ++i) {
+      const size_t npix = (size_t)probs[i].B * probs[i].H * probs[i].W;
+      if (npix > big) big = npix;
+    }
+    // fp32 large grids: 8 channels per thread; fp16 large grids: 4 groups of 2; else 4 x 1
+    const int cpt = (big >= 16384) ? 8 : 4;
+    cb8 = big >= 16384;
+    for (int i = i0; i < count && i < i0 + kWarpGroupMax; ++i) {
+      const WarpProblem& q = probs[i];
+      const size_t npix = (size_t)q.B * q.H * q.W;
+      if (npix == 0 || q.C == 0) continue;
+      if (npix * (size_t)(q.C > 2 ? q.C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
+      const unsigned gx = (unsigned)((npix + 255) / 256);
+      const unsigned gy = (unsigned)((q.C + cpt - 1) / cpt);
+      if ((unsigned long long)total + (unsigned long long)gx * gy >= (1ull << 31))
+        return hipErrorInvalidValue;
+      a.x[n] = (const T*)q.x;
+      a.flow[n] = (const T*)q.flow;
+      a.out[n] = (T*)q.out;
+      a.B[n] = q.B, a.C[n] = q.C, a.H[n] = q.H, a.W[n] = q.W;
+      a.halfx[n] = (float)((q.W - 1.0) / 2.0);
+      a.halfy[n] = (float)((q.H - 1.0) / 2.0);
+      a.gx[n] = gx;
+      a.start[n] = total;
+      total += gx * gy;
+      ++n;
+    }
+    if (n == 0) continue;
+    a.start[n] = total;
+    a.n = n;
+    if (!cb8)
+      hipLaunchKernelGGL((warp_fwd_group<T, 4, 1>), dim3(total), dim3(256), 0, stream, a);
+    else if (sizeof(T) == 4)
+      hipLaunchKernelGGL((warp_fwd_group<T, 8, 1>), dim3(total), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((warp_fwd_group<T, 2, 4>), dim3(total), dim3(256), 0, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+template hipError_t warp_forward_group_t<float>(const WarpProblem*, int, hipStream_t);
+template hipError_t warp_forward_group_t<__half>(const WarpProblem*, int, hipStream_t);
+template hipError_t warp_forward_group_t<__hip_bfloat16>(const WarpProblem*, int, hipStream_t);
 
 hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, void* gx,
                              void* gflow, int B, int C, int H, int W, hipStream_t stream) {

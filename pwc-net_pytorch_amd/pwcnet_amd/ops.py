@@ -272,6 +272,37 @@ def warp_forward(x, flow):
     return out
 
 
+def warp_forward_group(problems):
+    """[x2_warp] for a list of INDEPENDENT (x, flow) problems -- ``warp_forward`` each, bit
+    for bit, in one launch per 4 problems (pwc_warp_forward_group).  Inside one model forward
+    each level's warp needs the previous level's flow, so those levels are not a group."""
+    if not problems:
+        return []
+    items, dt = [], None
+    for (x, flow) in problems:
+        _check_inputs("WarpingLayer", x, flow)
+        B, C, H, W = x.shape
+        if tuple(flow.shape) != (B, 2, H, W):
+            raise ValueError(f"WarpingLayer: flow shape {tuple(flow.shape)} != {(B, 2, H, W)}")
+        if x.device != problems[0][0].device:
+            raise ValueError("WarpingLayer group: problems on different devices")
+        code = _lib.DTYPE_CODES[x.dtype]
+        if dt is not None and code != dt:
+            raise ValueError("WarpingLayer group: problems of different dtypes")
+        dt = code
+        _i32(B, C, H, W, x.numel())
+        x, flow = x.contiguous(), flow.contiguous()
+        items.append((x, flow, torch.empty_like(x)))
+    arr = (_lib.WarpProblem * len(items))()
+    for i, (x, f, o) in enumerate(items):
+        B, C, H, W = x.shape
+        arr[i] = _lib.WarpProblem(x.data_ptr(), f.data_ptr(), o.data_ptr(), B, C, H, W)
+    _lib.check(_lib.load().pwc_warp_forward_group(arr, len(items), dt,
+                                                  _stream(items[0][0].device)),
+               "WarpingLayer_forward_group")
+    return [o for (_, _, o) in items]
+
+
 def warp_backward(x, flow, grad_output):
     _check_inputs("WarpingLayer backward", x, flow, grad_output, dtypes=(torch.float32,))
     B, C, H, W = x.shape

@@ -150,3 +150,25 @@ def test_group_entry_host_checks():
     assert b"invalid correlation parameters" in lib.pwc_last_error()
     # an empty list is a no-op
     assert lib.pwc_warp_corr_forward_group(None, 0, 9, 1, 9, 1, 2, 1, 0, None) == 1
+
+
+def test_warp_group_entry_host_checks():
+    """pwc_warp_forward_group rejects a bad list before any launch: negative count, a NULL
+    list, a negative dimension, a NULL buffer, an unknown dtype; an empty list is a no-op."""
+    from pwcnet_amd import _lib
+    lib = _lib.load()
+    P = _lib.WarpProblem
+    assert lib.pwc_warp_forward_group(None, -1, 0, None) == 0
+    assert b"invalid problem list" in lib.pwc_last_error()
+    assert lib.pwc_warp_forward_group(None, 1, 0, None) == 0
+    arr = (P * 1)(P(1, 1, 1, -1, 4, 6, 7))
+    assert lib.pwc_warp_forward_group(arr, 1, 0, None) == 0
+    assert b"negative dimension" in lib.pwc_last_error()
+    arr = (P * 1)(P(1, 1, None, 1, 4, 6, 7))
+    assert lib.pwc_warp_forward_group(arr, 1, 0, None) == 0
+    assert b"null buffer" in lib.pwc_last_error()
+    arr = (P * 1)(P(1, 1, 1, 0, 4, 6, 7))  # empty batch: nothing to launch
+    assert lib.pwc_warp_forward_group(arr, 1, 7, None) == 0
+    assert b"unsupported dtype" in lib.pwc_last_error()
+    assert lib.pwc_warp_forward_group(None, 0, 0, None) == 1
+    assert lib.pwc_warp_forward_group(arr, 1, 0, None) == 1

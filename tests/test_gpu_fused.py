@@ -228,3 +228,33 @@ def test_fused_group_pair_disabled_is_identical():
         _lib.set_debug("")
     for (p, q), (r, s) in zip(o1, o2):
         assert torch.equal(p, r) and torch.equal(q, s)
+
+
+# grouped warps: lists of independent (x, flow) problems (pwc_warp_forward_group)
+WARP_GROUPS = [
+    [(8, 96, 24, 28), (8, 64, 48, 56), (8, 32, 96, 112)],  # the bench's l2 + l3 + l4
+    [(2, 32, 96, 112), (2, 96, 24, 28)],                   # largest first
+    [(1, 8, 5, 3), (2, 16, 7, 9), (0, 8, 6, 7), (1, 40, 11, 30), (3, 3, 9, 4),
+     (1, 12, 2, 2)],                                       # ragged, an empty batch, 2 launches
+    [(2, 192, 6, 7)],                                      # a single problem
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16], ids=["fp32", "fp16"])
+@pytest.mark.parametrize("group", WARP_GROUPS, ids=lambda g: "+".join(
+    "B{}C{}_{}x{}".format(*s) for s in g))
+def test_warp_group_matches_single_calls(group, dtype):
+    """Each problem of a grouped warp launch equals its own warp_forward call bit for bit
+    (same fmaf chain per element), and the oracle at 1e-5 (fp32; fp16 storage at 2e-3)."""
+    from pwcnet_amd.ops import warp_forward, warp_forward_group
+    data = [_inputs(_seed("wgroup", i, s), *s) for i, s in enumerate(group)]
+    probs = [(_t(b, dtype), _t(f, dtype)) for (_, b, f) in data]
+    outs = warp_forward_group(probs)
+    torch.cuda.synchronize()
+    assert len(outs) == len(group)
+    for (_, b, f), (x, fl), out in zip(data, probs, outs):
+        assert torch.equal(out, warp_forward(x, fl))
+        if b.shape[0] > 0 and b.size <= 2 * 96 * 24 * 28:
+            ref = O.warp_forward(_np(x), _np(fl))
+            tol = 1e-5 if dtype == torch.float32 else 2e-3
+            np.testing.assert_allclose(_np(out), ref, rtol=tol, atol=tol)
