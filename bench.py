@@ -119,6 +119,10 @@ def parse_args(argv=None):
                     help="issue the fused levels as one group (pwc_warp_corr_forward_group: "
                          "the bench's levels take independent inputs, so l0 + l1 share one "
                          "launch); off = one call per level")
+    ap.add_argument("--corr-group", default="on", choices=["on", "off"],
+                    help="the unfused levels' correlations below l4 (l2, l3) as one "
+                         "pwc_corr_forward_group launch (independent inputs); off = one call "
+                         "per level")
     ap.add_argument("--warp-group", default="on", choices=["on", "off"],
                     help="the unfused levels' warps (l2, l3, l4) as one pwc_warp_forward_group "
                          "launch ahead of their correlations (independent inputs); off = one "
@@ -200,7 +204,7 @@ class HipPass:
     P = (CORR_ARGS["pad_size"], CORR_ARGS["kernel_size"], CORR_ARGS["max_displacement"],
          CORR_ARGS["stride1"], CORR_ARGS["stride2"])
 
-    def __init__(self, dev, dtype, fused, group=False, warp_group=False):
+    def __init__(self, dev, dtype, fused, group=False, warp_group=False, corr_group=False):
         from pwcnet_amd import _lib
         from pwcnet_amd.ops import corr_forward, warp_forward
         self._lib = _lib
@@ -209,6 +213,7 @@ class HipPass:
         self.dev, self.dtype, self.fused = dev, dtype, fused
         self.group = group
         self.warp_group = warp_group
+        self.corr_group = corr_group
         self.dcode = _lib.DTYPE_CODES[dtype]
 
     def bind(self, s):
@@ -240,6 +245,7 @@ class HipPass:
         calls = []
         grouped = self.grouped_levels(s)
         wg = self.warp_levels(s)
+        cg = self.corr_levels(s)
         for l, lv in enumerate(s):
             B, C, h, w = lv["x1"].shape
             dims = [c_int(B), c_int(C), c_int(h), c_int(w)]
@@ -259,6 +265,11 @@ class HipPass:
                     calls.append((L.pwc_warp_corr_forward_group,
                                   (arr, c_int(len(grouped)), *cp, c_int(1), c_int(self.dcode),
                                    sp), f"levels {grouped}"))
+            elif l in cg:
+                if l == cg[0]:
+                    calls.append((L.pwc_corr_forward_group,
+                                  (self.corr_array(s, cg), c_int(len(cg)), *cp, c_int(1),
+                                   c_int(self.dcode), sp), f"corr levels {cg}"))
             elif l in self.fused:
                 calls.append((L.pwc_warp_corr_forward,
                               (p(lv["x1"]), p(lv["x2"]), p(lv["flow"]), p(lv["x2w"]),
@@ -304,6 +315,27 @@ class HipPass:
         lv = [l for l in range(len(s)) if l == len(s) - 1 or l not in self.fused]
         return lv if self.warp_group and len(lv) >= 2 else []
 
+    def corr_levels(self, s):
+        """The unfused levels below the last whose correlations run as one
+        pwc_corr_forward_group call (after their warps: needs the warp group too)."""
+        lv = [l for l in range(len(s) - 1) if l not in self.fused]
+        ok = self.corr_group and self.warp_levels(s) and len(lv) >= 2
+        return lv if ok else []
+
+    def corr_array(self, s, levels):
+        key = ("corrs", tuple(levels))
+        arr = s[0].get(key)
+        if arr is None:
+            T = self._lib.CorrProblem
+            arr = (T * len(levels))()
+            for i, l in enumerate(levels):
+                lv = s[l]
+                B, C, h, w = lv["x1"].shape
+                arr[i] = T(lv["x1"].data_ptr(), lv["x2w"].data_ptr(), lv["corr"].data_ptr(),
+                           B, C, h, w)
+            s[0][key] = arr
+        return arr
+
     def warp_array(self, s, levels):
         key = ("warps", tuple(levels))
         arr = s[0].get(key)
@@ -343,6 +375,7 @@ class HipPass:
         L, P, p = self.lib, self.P, self._p
         grouped = self.grouped_levels(s)
         wg = self.warp_levels(s)
+        cg = self.corr_levels(s)
         for l, lv in enumerate(s[:-1]):
             B, C, h, w = lv["x1"].shape
             if wg and l == wg[0]:
@@ -350,7 +383,12 @@ class HipPass:
                                                self.sp)
                 if ret != 1:
                     self._lib.check(ret, f"bench warps {wg}")
-            if l in grouped:
+            if l in cg:
+                ret = 1
+                if l == cg[0]:
+                    ret = L.pwc_corr_forward_group(self.corr_array(s, cg), len(cg), *P, 1,
+                                                   self.dcode, self.sp)
+            elif l in grouped:
                 ret = 1
                 if l == grouped[0]:
                     ret = L.pwc_warp_corr_forward_group(self.group_array(s, grouped),
@@ -708,7 +746,8 @@ def main(argv=None):
         nsets = 1
     else:
         pass_ = HipPass(dev, dtype, fused, group=args.group == "on",
-                        warp_group=args.warp_group == "on")
+                        warp_group=args.warp_group == "on",
+                        corr_group=args.corr_group == "on")
         per_set = sum((2 * C * h * w + 2 * h * w + 81 * h * w + C * h * w) * B * esz
                       for C, h, w in shapes)
         nsets = args.sets or max(2, int(np.ceil(2 * 256 * 2 ** 20 / per_set)))
@@ -849,6 +888,7 @@ def main(argv=None):
             "fused_levels": sorted(fused),
             "grouped_levels": (pass_.grouped_levels(shapes) if not cpu else []),
             "warp_grouped_levels": (pass_.warp_levels(shapes) if not cpu else []),
+            "corr_grouped_levels": (pass_.corr_levels(shapes) if not cpu else []),
             "graph": bool(graphs),
             "timing": timing,
             "device": "cpu (launcher rehearsal: torch-CPU stand-in, not the product path)"

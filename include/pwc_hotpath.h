@@ -216,6 +216,23 @@ PWC_API int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, i
                                         int pad_size, int kernel_size, int max_displacement,
                                         int stride1, int stride2, int corr_multiply, int dtype,
                                         void* stream);
+/* Several INDEPENDENT correlations (e.g. the bench's synthetic pyramid levels, or the levels
+ * of different batches in flight; inside one model forward each level's correlation needs that
+ * level's warp, which needs the previous level's flow).  Each problem's output equals a
+ * pwc_corr_forward call on it, bit for bit; problems of model.py:24's configuration in fp32
+ * that take the row-band kernel (l2 + l3 at 384x448) are paired into ONE launch (one workgroup
+ * per CU; the second grid fills the CUs the first leaves idle), the rest run one
+ * pwc_corr_forward call each.  Replaces a sequence of Correlation calls
+ * (correlation_cuda.c:36-90 per call); returns 1 on success. */
+typedef struct {
+  const void* in1;
+  const void* in2;
+  void* out;
+  int B, C, H, W;
+} pwc_corr_problem;
+PWC_API int pwc_corr_forward_group(const pwc_corr_problem* problems, int count, int pad_size,
+                                   int kernel_size, int max_displacement, int stride1,
+                                   int stride2, int corr_multiply, int dtype, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -32,6 +32,9 @@ hipError_t warp_backward_f32(const void*, const void*, const void*, void*, void*
 template <typename T>
 hipError_t upsample_warp_forward_t(const void*, const void*, void*, void*, int, int, int, int,
                                    hipStream_t);
+hipError_t corr_forward_rows_pair(const void*, const void*, void*, int, int, int, int,
+                                  const void*, const void*, void*, int, int, int, int, float,
+                                  float, hipStream_t);
 hipError_t flow_up2_backward_f32(const void*, void*, int, int, int, hipStream_t);
 hipError_t warp_corr_band_pair_f32(const BandProblem& a, const BandProblem& b, float divisor_a,
                                    float divisor_b, hipStream_t stream);
@@ -672,3 +675,63 @@ int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, int count
 }
 
 }  // extern "C"
+
+// ---- grouped correlation (independent problems; the bench's l2 + l3) ----
+// A problem the row-band kernel takes in a single call: model.py:24's configuration in fp32,
+// rows too narrow for the stream kernel (W < 64), too many for the band kernel ((H+1)/2 > 6),
+// 16-B aligned buffers (corr_fwd.hip's dispatch order: stream, band, rows).
+static bool rows_pairable(const pwc_corr_problem& q, int pad, int k, int md, int s1, int s2,
+                          int dtype) {
+  return dtype == PWC_DTYPE_F32 && k == 1 && s1 == 1 && s2 == 2 && pad == md &&
+         (md == 8 || md == 9) && force_generic() == 0 && q.W < 64 && (q.H + 1) / 2 > 6 &&
+         (size_t)q.B * q.C * q.H * q.W > 0 && (uintptr_t)q.in1 % 16 == 0 &&
+         (uintptr_t)q.in2 % 16 == 0 && (uintptr_t)q.out % 16 == 0;
+}
+
+int pwc_corr_forward_group(const pwc_corr_problem* problems, int count, int pad_size,
+                           int kernel_size, int max_displacement, int stride1, int stride2,
+                           int corr_multiply, int dtype, void* stream) {
+  const char* fn = "pwc_corr_forward_group";
+  if (count < 0 || (count > 0 && !problems)) return fail(fn, "invalid problem list");
+  for (int i = 0; i < count; ++i) {
+    const pwc_corr_problem& q = problems[i];
+    int OC, Ho, Wo;
+    if (!dims_ok(q.B, q.C, q.H, q.W)) return fail(fn, "negative dimension");
+    if (!corr_shape(q.H, q.W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC,
+                    &Ho, &Wo))
+      return fail(fn, "invalid correlation parameters");
+    if ((size_t)q.B * q.C * q.H * q.W && (!q.in1 || !q.in2 || !q.out))
+      return fail(fn, "null buffer");
+  }
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<char> done((size_t)count, 0);
+  int open = -1;
+  for (int i = 0; i < count; ++i) {
+    const pwc_corr_problem& q = problems[i];
+    if (!rows_pairable(q, pad_size, kernel_size, max_displacement, stride1, stride2, dtype))
+      continue;
+    if (open < 0) {
+      open = i;
+      continue;
+    }
+    const pwc_corr_problem& p = problems[open];
+    const hipError_t e = pwc::corr_forward_rows_pair(
+        p.in1, p.in2, p.out, p.B, p.C, p.H, p.W, q.in1, q.in2, q.out, q.B, q.C, q.H, q.W,
+        (float)p.C, (float)q.C, s);
+    if (e == hipErrorNotSupported) {
+      open = i;
+      continue;
+    }
+    if (!check_launch(fn, e)) return 0;
+    done[(size_t)open] = done[(size_t)i] = 1;
+    open = -1;
+  }
+  for (int i = 0; i < count; ++i) {
+    if (done[(size_t)i]) continue;
+    const pwc_corr_problem& q = problems[i];
+    if (!pwc_corr_forward(q.in1, q.in2, q.out, q.B, q.C, q.H, q.W, pad_size, kernel_size,
+                          max_displacement, stride1, stride2, corr_multiply, dtype, stream))
+      return 0;
+  }
+  return 1;
+}

@@ -70,19 +70,18 @@ __device__ __forceinline__ void lds_barrier() {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
+// One workgroup's band (`unit0` = its XCD-remapped index within its problem's grid).
 template <typename T, int R, int NT, int ML1, int ML2>
-__global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
-                                                       const T* __restrict__ f2,
-                                                       T* __restrict__ out, int C, int H,
-                                                       int W, float divisor, float inv_divisor,
-                                                       Geo g, OutEpi epi) {
+__device__ __forceinline__ void rows_band(const T* __restrict__ f1, const T* __restrict__ f2,
+                                          T* __restrict__ out, int C, int H, int W,
+                                          float divisor, float inv_divisor, const Geo& g,
+                                          const OutEpi& epi, const int unit0) {
   constexpr bool H16 = sizeof(T) == 2;
   constexpr int EPQ = 16 / (int)sizeof(T);  // pixels per 16-B quad
   constexpr int HPQ = EPQ / 2;              // parity slots per quad and column parity
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int NR2 = g.NR2;
   const int t = threadIdx.x;
-  const int unit0 = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring bands share an L2
   const int tg = unit0 % g.TS, unit = unit0 / g.TS;    // displacement-row group
   const int tj0 = tg * g.DT;
   const int b = unit % g.nb, np = unit / g.nb;
@@ -270,15 +269,59 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
   }
 }
 
+template <typename T, int R, int NT, int ML1, int ML2>
+__global__ __launch_bounds__(NT, 1) void corr_fwd_rows(const T* __restrict__ f1,
+                                                       const T* __restrict__ f2,
+                                                       T* __restrict__ out, int C, int H,
+                                                       int W, float divisor, float inv_divisor,
+                                                       Geo g, OutEpi epi) {
+  // neighbouring bands share an L2
+  rows_band<T, R, NT, ML1, ML2>(f1, f2, out, C, H, W, divisor, inv_divisor, g, epi,
+                                xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// Two INDEPENDENT problems in one launch (pwc_corr_forward_group): blocks [0, nA) run problem
+// A's bands, the rest problem B's, each remapped over its own grid.  One workgroup per CU
+// either way (LDS = the larger plan's), so the pair shares one launch gap and B's bands fill
+// the CUs A's smaller grid leaves idle.
+struct RowsArgs {
+  const void* f1;
+  const void* f2;
+  void* out;
+  int C, H, W;
+  float divisor, inv;
+  Geo g;
+};
+
+template <typename T, int RA, int M1A, int M2A, int RB, int M1B, int M2B, int NT>
+__global__ __launch_bounds__(NT, 1) void corr_fwd_rows_pair(RowsArgs a, RowsArgs b, int nA,
+                                                            OutEpi epi) {
+  const int bid = blockIdx.x;
+  if (bid < nA)
+    rows_band<T, RA, NT, M1A, M2A>((const T*)a.f1, (const T*)a.f2, (T*)a.out, a.C, a.H, a.W,
+                                   a.divisor, a.inv, a.g, epi, xcd_remap(bid, nA));
+  else
+    rows_band<T, RB, NT, M1B, M2B>((const T*)b.f1, (const T*)b.f2, (T*)b.out, b.C, b.H, b.W,
+                                   b.divisor, b.inv, b.g, epi,
+                                   xcd_remap(bid - nA, (int)gridDim.x - nA));
+}
+
 }  // namespace rows
 
 // Serves l3-sized grids (13..24 parity rows per image) by default.  PWC_ROWS=0 disables the
 // kernel, PWC_ROWS=1 selects it at every size >= 13 parity rows, PWC_ROWS_CFG="R,CK" forces
 // a configuration at any size (measurement).
 // dtype 0: fp32 storage, 1: fp16 (Sintel l0..l2 of config 4: every parity-row count, W % 8).
-hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B, int C, int H,
-                             int W, float divisor, int dtype, hipStream_t stream) {
-  using namespace rows;
+namespace rows {
+struct Plan {
+  Geo g;
+  size_t lds;
+  int R, per1, per2;
+  float inv;
+  bool h16;
+};
+
+static hipError_t plan(int B, int C, int H, int W, float divisor, int dtype, Plan* P) {
   const int mode = debug_knob("rows", 1);  // 0 off, 2 forced at every size (measurement)
   if (mode == 0 || (dtype != 0 && dtype != 1)) return hipErrorNotSupported;
   const bool h16 = dtype == 1;
@@ -351,6 +394,29 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
   int ex;
   const float mnt = std::frexp(divisor, &ex);
   const float inv = (mnt == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
+  P->g = g;
+  P->lds = lds;
+  P->R = R;
+  P->per1 = per1;
+  P->per2 = per2;
+  P->inv = inv;
+  P->h16 = h16;
+  return hipSuccess;
+}
+}  // namespace rows
+
+hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B, int C, int H,
+                             int W, float divisor, int dtype, hipStream_t stream) {
+  using namespace rows;
+  Plan P;
+  const hipError_t pe = plan(B, C, H, W, divisor, dtype, &P);
+  if (pe != hipSuccess) return pe;
+  const Geo& g = P.g;
+  const size_t lds = P.lds;
+  const int R = P.R, per1 = P.per1, per2 = P.per2;
+  const float inv = P.inv;
+  const bool h16 = P.h16;
+  constexpr int NT = 768;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);
 #define PWC_ROWS(TT, RR, M1, M2)                                                              \
@@ -381,6 +447,60 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
   PWC_ROWS(_Float16, 1, 1, 3)
   PWC_ROWS(_Float16, 1, 2, 5)
 #undef PWC_ROWS
+  return hipErrorNotSupported;
+}
+
+// Two independent fp32 problems that each take the row-band kernel, as one launch; the
+// variant pairs instantiated are the config-2 l2 (R 1) + l3 (R 3) ones.  hipErrorNotSupported
+// = no such pair (the caller runs them one by one).  Values equal the single launches bit for
+// bit (same workgroup body and plan).
+hipError_t corr_forward_rows_pair(const void* a1, const void* a2, void* aout, int aB, int aC,
+                                  int aH, int aW, const void* b1, const void* b2, void* bout,
+                                  int bB, int bC, int bH, int bW, float adiv, float bdiv,
+                                  hipStream_t stream) {
+  using namespace rows;
+  if (!epi_is_default(current_epi()) || debug_knob("rows_pair", 1) == 0)
+    return hipErrorNotSupported;
+  Plan pa, pb;
+  if (plan(aB, aC, aH, aW, adiv, 0, &pa) != hipSuccess ||
+      plan(bB, bC, bH, bW, bdiv, 0, &pb) != hipSuccess)
+    return hipErrorNotSupported;
+  const long long nA = pa.g.units, nB = pb.g.units;
+  if (nA + nB >= (1ll << 31)) return hipErrorNotSupported;
+  const size_t lds = pa.lds > pb.lds ? pa.lds : pb.lds;
+  const RowsArgs A{a1, a2, aout, aC, aH, aW, adiv, pa.inv, pa.g};
+  const RowsArgs Bq{b1, b2, bout, bC, bH, bW, bdiv, pb.inv, pb.g};
+  constexpr int NT = 768;
+#define PWC_ROWS_PAIR(RA, M1A, M2A, RB, M1B, M2B)                                             \
+  if (pa.R == RA && pa.per1 <= M1A && pa.per2 <= M2A && pb.R == RB && pb.per1 <= M1B &&       \
+      pb.per2 <= M2B) {                                                                       \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      hipError_t e = hipFuncSetAttribute(                                                     \
+          reinterpret_cast<const void*>(                                                      \
+              &corr_fwd_rows_pair<float, RA, M1A, M2A, RB, M1B, M2B, NT>),                    \
+          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+      if (e != hipSuccess) return e;                                                          \
+      attr = true;                                                                            \
+    }                                                                                         \
+    hipLaunchKernelGGL((corr_fwd_rows_pair<float, RA, M1A, M2A, RB, M1B, M2B, NT>),           \
+                       dim3((unsigned)(nA + nB)), dim3(NT), lds, stream, A, Bq, (int)nA,      \
+                       current_epi());                                                        \
+    return hipGetLastError();                                                                 \
+  }
+  // the variants the single launcher would pick (same first-match order: R 3 takes (2, 7)
+  // before (1, 4); R 1 takes (1, 5))
+  const bool a3 = pa.R == 3 && pa.per1 <= 2 && pa.per2 <= 7;
+  const bool b3 = pb.R == 3 && pb.per1 <= 2 && pb.per2 <= 7;
+  const bool a1v = pa.R == 1 && pa.per1 <= 1 && pa.per2 <= 5;
+  const bool b1v = pb.R == 1 && pb.per1 <= 1 && pb.per2 <= 5;
+  if (a1v && b3) {
+    PWC_ROWS_PAIR(1, 1, 5, 3, 2, 7)
+  }
+  if (a3 && b1v) {
+    PWC_ROWS_PAIR(3, 2, 7, 1, 1, 5)
+  }
+#undef PWC_ROWS_PAIR
   return hipErrorNotSupported;
 }
 

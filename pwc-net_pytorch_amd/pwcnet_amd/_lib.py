@@ -42,6 +42,12 @@ class WarpProblem(ctypes.Structure):
                 ("W", _I)]
 
 
+class CorrProblem(ctypes.Structure):
+    """pwc_corr_problem (include/pwc_hotpath.h)."""
+    _fields_ = [("in1", _P), ("in2", _P), ("out", _P), ("B", _I), ("C", _I), ("H", _I),
+                ("W", _I)]
+
+
 SYMBOLS = {
     "pwc_abi_version": (_I, []),
     "pwc_last_error": (ctypes.c_char_p, []),
@@ -61,6 +67,7 @@ SYMBOLS = {
     "pwc_warp_corr_workspace_size": (_Z, [_I] * 11),
     "pwc_warp_corr_forward": (_I, [_P] * 5 + [_I] * 11 + [_P, _Z, _P]),
     "pwc_warp_corr_forward_group": (_I, [ctypes.POINTER(WarpCorrProblem)] + [_I] * 8 + [_P]),
+    "pwc_corr_forward_group": (_I, [ctypes.POINTER(CorrProblem)] + [_I] * 8 + [_P]),
     "pwc_warp_forward_group": (_I, [ctypes.POINTER(WarpProblem), _I, _I, _P]),
     "pwc_upsample_warp_forward": (_I, [_P] * 4 + [_I] * 5 + [_P]),
     "pwc_flow_upsample_backward": (_I, [_P, _P] + [_I] * 4 + [_P]),

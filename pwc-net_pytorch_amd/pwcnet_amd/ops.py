@@ -303,6 +303,42 @@ def warp_forward_group(problems):
     return [o for (_, _, o) in items]
 
 
+def corr_forward_group(problems, pad_size, kernel_size, max_displacement, stride1, stride2,
+                       corr_multiply=1):
+    """[corr] for a list of INDEPENDENT (input1, input2) problems -- ``corr_forward`` each,
+    bit for bit; fp32 problems of model.py:24's configuration that take the row-band kernel
+    (l2 + l3 at 384x448) are paired into one launch (pwc_corr_forward_group)."""
+    if not problems:
+        return []
+    items, dt = [], None
+    for (input1, input2) in problems:
+        _check_inputs("Correlation", input1, input2)
+        if input1.shape != input2.shape:
+            raise ValueError(f"Correlation: input shapes differ {tuple(input1.shape)} vs "
+                             f"{tuple(input2.shape)}")
+        if input1.device != problems[0][0].device:
+            raise ValueError("Correlation group: problems on different devices")
+        code = _lib.DTYPE_CODES[input1.dtype]
+        if dt is not None and code != dt:
+            raise ValueError("Correlation group: problems of different dtypes")
+        dt = code
+        B, C, H, W = input1.shape
+        _i32(B, C, H, W, input1.numel())
+        input1, input2 = input1.contiguous(), input2.contiguous()
+        OC, Ho, Wo = _lib.corr_output_shape(H, W, pad_size, kernel_size, max_displacement,
+                                            stride1, stride2)
+        out = torch.empty((B, OC, Ho, Wo), dtype=input1.dtype, device=input1.device)
+        items.append((input1, input2, out))
+    arr = (_lib.CorrProblem * len(items))()
+    for i, (a, b, o) in enumerate(items):
+        B, C, H, W = a.shape
+        arr[i] = _lib.CorrProblem(a.data_ptr(), b.data_ptr(), o.data_ptr(), B, C, H, W)
+    _lib.check(_lib.load().pwc_corr_forward_group(
+        arr, len(items), pad_size, kernel_size, max_displacement, stride1, stride2,
+        corr_multiply, dt, _stream(items[0][0].device)), "Correlation_forward_group")
+    return [o for (_, _, o) in items]
+
+
 def warp_backward(x, flow, grad_output):
     _check_inputs("WarpingLayer backward", x, flow, grad_output, dtypes=(torch.float32,))
     B, C, H, W = x.shape

@@ -172,3 +172,24 @@ def test_warp_group_entry_host_checks():
     assert b"unsupported dtype" in lib.pwc_last_error()
     assert lib.pwc_warp_forward_group(None, 0, 0, None) == 1
     assert lib.pwc_warp_forward_group(arr, 1, 0, None) == 1
+
+
+def test_corr_group_entry_host_checks():
+    """pwc_corr_forward_group rejects a bad list before any launch: negative count, a NULL
+    list, a negative dimension, a NULL buffer, invalid correlation parameters."""
+    from pwcnet_amd import _lib
+    lib = _lib.load()
+    P = _lib.CorrProblem
+    assert lib.pwc_corr_forward_group(None, -1, 9, 1, 9, 1, 2, 1, 0, None) == 0
+    assert b"invalid problem list" in lib.pwc_last_error()
+    assert lib.pwc_corr_forward_group(None, 1, 9, 1, 9, 1, 2, 1, 0, None) == 0
+    arr = (P * 1)(P(1, 1, 1, -1, 4, 6, 7))
+    assert lib.pwc_corr_forward_group(arr, 1, 9, 1, 9, 1, 2, 1, 0, None) == 0
+    assert b"negative dimension" in lib.pwc_last_error()
+    arr = (P * 1)(P(1, None, 1, 1, 4, 6, 7))
+    assert lib.pwc_corr_forward_group(arr, 1, 9, 1, 9, 1, 2, 1, 0, None) == 0
+    assert b"null buffer" in lib.pwc_last_error()
+    arr = (P * 1)(P(1, 1, 1, 1, 4, 6, 7))
+    assert lib.pwc_corr_forward_group(arr, 1, 9, 1, 9, 1, 0, 1, 0, None) == 0
+    assert b"invalid correlation parameters" in lib.pwc_last_error()
+    assert lib.pwc_corr_forward_group(None, 0, 9, 1, 9, 1, 2, 1, 0, None) == 1

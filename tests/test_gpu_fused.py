@@ -258,3 +258,56 @@ def test_warp_group_matches_single_calls(group, dtype):
             ref = O.warp_forward(_np(x), _np(fl))
             tol = 1e-5 if dtype == torch.float32 else 2e-3
             np.testing.assert_allclose(_np(out), ref, rtol=tol, atol=tol)
+
+
+# grouped correlations (pwc_corr_forward_group): the row-band pair and the one-by-one rest
+CORR_GROUPS = [
+    [(8, 96, 24, 28), (8, 64, 48, 56)],                  # the bench's l2 + l3: one paired launch
+    [(8, 64, 48, 56), (8, 96, 24, 28)],                  # the other order
+    [(2, 192, 6, 7), (2, 96, 24, 28), (1, 32, 96, 112), (2, 64, 48, 56)],  # band, pair, stream
+    [(1, 24, 13, 15), (0, 8, 6, 7), (2, 96, 24, 28)],    # ragged, an empty batch, one rows level
+]
+
+
+@pytest.mark.parametrize("group", CORR_GROUPS, ids=lambda g: "+".join(
+    "B{}C{}_{}x{}".format(*s) for s in g))
+def test_corr_group_matches_single_calls(group):
+    """Each problem of a grouped correlation equals its own corr_forward call bit for bit (the
+    pair kernel runs the row-band workgroup body on the same plan), and the oracle at 1e-5."""
+    import ctypes
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_forward_group
+    data = [_inputs(_seed("cgroup", i, s), *s) for i, s in enumerate(group)]
+    probs = [(_t(a), _t(b)) for (a, b, _) in data]
+    outs = corr_forward_group(probs, 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    assert len(outs) == len(group)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for (a, b, _), (x1, x2), out in zip(data, probs, outs):
+        ref = torch.empty_like(out)
+        if ref.numel():  # the single call the group promises to equal: pwc_corr_forward
+            B, C, H, W = x1.shape
+            assert _lib.load().pwc_corr_forward(
+                ctypes.c_void_p(x1.data_ptr()), ctypes.c_void_p(x2.data_ptr()),
+                ctypes.c_void_p(ref.data_ptr()), B, C, H, W, 9, 1, 9, 1, 2, 1, 0, stream) == 1
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        if a.shape[0] > 0 and a.size <= 2 * 96 * 24 * 28:
+            cref = O.corr_forward(a, b, 9, 1, 9, 1, 2)
+            np.testing.assert_allclose(_np(out), cref, rtol=1e-5, atol=1e-5)
+
+
+def test_corr_group_pair_disabled_is_identical():
+    """The pair kernel against the one-call-per-problem path of the same entry point."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_forward_group
+    data = [_inputs(31 + i, *s) for i, s in enumerate(CORR_GROUPS[0])]
+    probs = [(_t(a), _t(b)) for (a, b, _) in data]
+    o1 = corr_forward_group(probs, 9, 1, 9, 1, 2)
+    _lib.set_debug("rows_pair=0")
+    try:
+        o2 = corr_forward_group(probs, 9, 1, 9, 1, 2)
+    finally:
+        _lib.set_debug("")
+    for p, q in zip(o1, o2):
+        assert torch.equal(p, q)
