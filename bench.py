@@ -123,6 +123,9 @@ def parse_args(argv=None):
                     help="the unfused levels' correlations below l4 (l2, l3) as one "
                          "pwc_corr_forward_group launch (independent inputs); off = one call "
                          "per level")
+    ap.add_argument("--group-order", default="desc", choices=["asc", "desc"],
+                    help="problem order inside the warp / correlation groups: asc = l2 first, "
+                         "desc = the largest level's workgroups dispatched first")
     ap.add_argument("--warp-group", default="on", choices=["on", "off"],
                     help="the unfused levels' warps (l2, l3, l4) as one pwc_warp_forward_group "
                          "launch ahead of their correlations (independent inputs); off = one "
@@ -204,7 +207,8 @@ class HipPass:
     P = (CORR_ARGS["pad_size"], CORR_ARGS["kernel_size"], CORR_ARGS["max_displacement"],
          CORR_ARGS["stride1"], CORR_ARGS["stride2"])
 
-    def __init__(self, dev, dtype, fused, group=False, warp_group=False, corr_group=False):
+    def __init__(self, dev, dtype, fused, group=False, warp_group=False, corr_group=False,
+                 group_desc=False):
         from pwcnet_amd import _lib
         from pwcnet_amd.ops import corr_forward, warp_forward
         self._lib = _lib
@@ -214,6 +218,7 @@ class HipPass:
         self.group = group
         self.warp_group = warp_group
         self.corr_group = corr_group
+        self.group_desc = group_desc
         self.dcode = _lib.DTYPE_CODES[dtype]
 
     def bind(self, s):
@@ -250,7 +255,7 @@ class HipPass:
             B, C, h, w = lv["x1"].shape
             dims = [c_int(B), c_int(C), c_int(h), c_int(w)]
             cp = [c_int(v) for v in P]
-            if wg and l == wg[0]:
+            if wg and l == min(wg):
                 calls.append((L.pwc_warp_forward_group,
                               (self.warp_array(s, wg), c_int(len(wg)), c_int(self.dcode), sp),
                               f"warps {wg}"))
@@ -266,7 +271,7 @@ class HipPass:
                                   (arr, c_int(len(grouped)), *cp, c_int(1), c_int(self.dcode),
                                    sp), f"levels {grouped}"))
             elif l in cg:
-                if l == cg[0]:
+                if l == min(cg):
                     calls.append((L.pwc_corr_forward_group,
                                   (self.corr_array(s, cg), c_int(len(cg)), *cp, c_int(1),
                                    c_int(self.dcode), sp), f"corr levels {cg}"))
@@ -313,14 +318,15 @@ class HipPass:
     def warp_levels(self, s):
         """The unfused levels whose warps run as one pwc_warp_forward_group call."""
         lv = [l for l in range(len(s)) if l == len(s) - 1 or l not in self.fused]
-        return lv if self.warp_group and len(lv) >= 2 else []
+        ok = self.warp_group and len(lv) >= 2
+        return (lv[::-1] if self.group_desc else lv) if ok else []
 
     def corr_levels(self, s):
         """The unfused levels below the last whose correlations run as one
         pwc_corr_forward_group call (after their warps: needs the warp group too)."""
         lv = [l for l in range(len(s) - 1) if l not in self.fused]
         ok = self.corr_group and self.warp_levels(s) and len(lv) >= 2
-        return lv if ok else []
+        return (lv[::-1] if self.group_desc else lv) if ok else []
 
     def corr_array(self, s, levels):
         key = ("corrs", tuple(levels))
@@ -378,14 +384,14 @@ class HipPass:
         cg = self.corr_levels(s)
         for l, lv in enumerate(s[:-1]):
             B, C, h, w = lv["x1"].shape
-            if wg and l == wg[0]:
+            if wg and l == min(wg):
                 ret = L.pwc_warp_forward_group(self.warp_array(s, wg), len(wg), self.dcode,
                                                self.sp)
                 if ret != 1:
                     self._lib.check(ret, f"bench warps {wg}")
             if l in cg:
                 ret = 1
-                if l == cg[0]:
+                if l == min(cg):
                     ret = L.pwc_corr_forward_group(self.corr_array(s, cg), len(cg), *P, 1,
                                                    self.dcode, self.sp)
             elif l in grouped:
@@ -747,7 +753,8 @@ def main(argv=None):
     else:
         pass_ = HipPass(dev, dtype, fused, group=args.group == "on",
                         warp_group=args.warp_group == "on",
-                        corr_group=args.corr_group == "on")
+                        corr_group=args.corr_group == "on",
+                        group_desc=args.group_order == "desc")
         per_set = sum((2 * C * h * w + 2 * h * w + 81 * h * w + C * h * w) * B * esz
                       for C, h, w in shapes)
         nsets = args.sets or max(2, int(np.ceil(2 * 256 * 2 ** 20 / per_set)))
