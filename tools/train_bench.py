@@ -22,8 +22,9 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from pwcnet_amd.ops import (corr_backward, corr_forward, warp_backward,  # noqa: E402
-                            warp_corr_forward, warp_forward)
+from pwcnet_amd.ops import (corr_backward, corr_forward, corr_forward_group,  # noqa: E402
+                            warp_backward, warp_corr_forward, warp_corr_forward_group,
+                            warp_forward, warp_forward_group)
 
 
 def main():
@@ -35,6 +36,10 @@ def main():
     ap.add_argument("--width", type=int, default=448)
     ap.add_argument("--fused-levels", default="0,1",
                     help="levels whose forward runs as one WarpCorrelation launch (as bench.py)")
+    ap.add_argument("--group", default="on", choices=["on", "off"],
+                    help="forward as bench.py's grouped launches (the levels' inputs are "
+                         "independent here): fused l0+l1 pair, one warp group, the row-band "
+                         "correlation pair; off = one call per level")
     args = ap.parse_args()
     fused = {int(v) for v in args.fused_levels.split(",") if v.strip()}
     dev = torch.device("cuda:0")
@@ -53,7 +58,29 @@ def main():
                           gc=torch.randn(B, 81, h, w, device=dev, generator=gen)))
         sets.append(s)
 
+    def forward_grouped(s):
+        last = len(s) - 1
+        fl = sorted(l for l in fused if l < last)
+        for l, (c, w) in zip(fl, warp_corr_forward_group(
+                [(s[l]["x1"], s[l]["x2"], s[l]["fl"]) for l in fl], **bench.CORR_ARGS)):
+            s[l]["corr"], s[l]["x2w"] = c, w
+        wl = [l for l in range(last, -1, -1) if l == last or l not in fused]
+        for l, w in zip(wl, warp_forward_group([(s[l]["x2"], s[l]["fl"]) for l in wl])):
+            s[l]["x2w"] = w
+        cl = [l for l in wl if l != last]
+        for l, c in zip(cl, corr_forward_group([(s[l]["x1"], s[l]["x2w"]) for l in cl],
+                                               **bench.CORR_ARGS)):
+            s[l]["corr"] = c
+        s[last]["corr"] = corr_forward(s[last]["x1"], s[last]["x2w"], **bench.CORR_ARGS)
+        for lv in s:
+            g1, g2w = corr_backward(lv["x1"], lv["x2w"], lv["gc"], **bench.CORR_ARGS)
+            lv["g1"] = g1
+            lv["gx2"], lv["gfl"] = warp_backward(lv["x2"], lv["fl"], g2w)
+
     def one(s):
+        if args.group == "on":
+            forward_grouped(s)
+            return
         for l, lv in enumerate(s):
             if l in fused:  # model.py:80-83 as one WarpCorrelation launch (emits x2_warp too)
                 lv["corr"], x2w = warp_corr_forward(lv["x1"], lv["x2"], lv["fl"],
@@ -92,7 +119,7 @@ def main():
         "data": "synthetic (randn features and cost-volume gradients, N(0,2^2) flows)",
         "config": {"workload": "BASELINE config 5: B=8 384x448 training step of the hot path",
                    "batch": B, "levels": [list(x) for x in shapes], "graph": True,
-                   "fused_levels": sorted(fused),
+                   "fused_levels": sorted(fused), "grouped": args.group == "on",
                    "buffer_sets": nsets}}), flush=True)
 
 
