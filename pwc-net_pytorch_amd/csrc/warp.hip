@@ -705,8 +705,9 @@ hipError_t warp_forward_group_t(const WarpProblem* probs, int count, hipStream_t
       if (npix > big) big = npix;
     }
     // fp32 large grids: 8 channels per thread; fp16 large grids: 4 groups of 2; else 4 x 1
-    const int cpt = (big >= 16384) ? 8 : 4;
-    cb8 = big >= 16384;
+    // knob warp_group_cpt=4 keeps 4 channels per thread on large grids (measurement)
+    cb8 = big >= 16384 && debug_knob("warp_group_cpt", 8) == 8;
+    const int cpt = cb8 ? 8 : 4;
     for (int i = i0; i < count && i < i0 + kWarpGroupMax; ++i) {
       const WarpProblem& q = probs[i];
       const size_t npix = (size_t)q.B * q.H * q.W;
