@@ -73,13 +73,13 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
                                                    const float* __restrict__ gout,
                                                    float* __restrict__ gin, int C, int H,
                                                    int W, float divisor, float inv_divisor,
-                                                   const Geo& g, const int unit,
-                                                   const int slice) {
+                                                   const Geo& g) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* stg = lds;
   f32x4* part = reinterpret_cast<f32x4*>(lds + g.stf);
   const int t = threadIdx.x;
   const int R = g.R, NR = R + 8;
+  const int unit = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring bands share an L2
   const int b = unit % g.nb, np = unit / g.nb;
   const int p = np & 1, n = np >> 1;
   const int hp = (H - p + 1) >> 1;
@@ -173,7 +173,7 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
 
   // channel slice of this workgroup (grid.y), chunks of ck; the next chunk's staging loads
   // are in flight during the current chunk's compute and epilogue
-  const int cs = slice * g.cps, ce = min(C, cs + g.cps);
+  const int cs = blockIdx.y * g.cps, ce = min(C, cs + g.cps);
   f32x4 vv[ML];
   float vs[ML];
   auto issue = [&](int cb) {
@@ -287,56 +287,11 @@ __global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__
                                                        float* __restrict__ g2, int C, int H,
                                                        int W, float divisor, float inv_divisor,
                                                        Geo g) {
-  const int unit = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring bands share an L2
   if (blockIdx.z == 0)
-    corr_bwd_rows_body<1, VEC, CT, ML, NT>(f2, gout, g1, C, H, W, divisor, inv_divisor, g, unit,
-                                           blockIdx.y);
+    corr_bwd_rows_body<1, VEC, CT, ML, NT>(f2, gout, g1, C, H, W, divisor, inv_divisor, g);
   else
-    corr_bwd_rows_body<2, VEC, CT, ML, NT>(f1, gout, g2, C, H, W, divisor, inv_divisor, g, unit,
-                                           blockIdx.y);
+    corr_bwd_rows_body<2, VEC, CT, ML, NT>(f1, gout, g2, C, H, W, divisor, inv_divisor, g);
 }
-
-// Two INDEPENDENT problems of one variant in one launch (the training step's l0 + l1, whose
-// grids are about one workgroup round each): flat blocks [0, nA) are problem A's
-// (unit, slice, gradient) grid, the rest B's.  Two workgroups per CU (launch bounds), so the
-// two latency-bound grids share the CUs.
-struct BwdArgs {
-  const float* f1;
-  const float* f2;
-  const float* gout;
-  float* g1;
-  float* g2;
-  int C, H, W;
-  float divisor, inv;
-  int units, nsl;
-  Geo g;
-};
-
-template <bool VEC, int CT, int ML, int NT>
-__device__ __forceinline__ void bwd_pair_item(const BwdArgs& a, int local) {
-  const int per = a.units * a.nsl;
-  const int z = local / per;
-  const int r = local - z * per;
-  const int y = r / a.units;
-  const int x = r - y * a.units;
-  const int unit = xcd_remap(x, a.units);
-  if (z == 0)
-    corr_bwd_rows_body<1, VEC, CT, ML, NT>(a.f2, a.gout, a.g1, a.C, a.H, a.W, a.divisor, a.inv,
-                                           a.g, unit, y);
-  else
-    corr_bwd_rows_body<2, VEC, CT, ML, NT>(a.f1, a.gout, a.g2, a.C, a.H, a.W, a.divisor, a.inv,
-                                           a.g, unit, y);
-}
-
-template <bool VEC, int CT, int ML, int NT>
-__global__ __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(6, 8))) void corr_bwd_rows_pair(BwdArgs a, BwdArgs b, int nA) {
-  const int bid = blockIdx.x;
-  if (bid < nA)
-    bwd_pair_item<VEC, CT, ML, NT>(a, bid);
-  else
-    bwd_pair_item<VEC, CT, ML, NT>(b, bid - nA);
-}
-template __global__ void corr_bwd_rows_pair<false, 2, 4, 768>(BwdArgs, BwdArgs, int);
 
 }  // namespace bwdrows
 
