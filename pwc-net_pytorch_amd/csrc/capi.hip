@@ -135,10 +135,8 @@ bool corr_shape(int H, int W, int pad, int k, int md, int s1, int s2, int* oc, i
   return true;
 }
 
-// Kernel-selection override for cross-checks (env PWC_CORR_PATH, read once):
-//   "generic" (1): literal one-thread-per-output kernels only;
-//   "regtile" (2): skip the LDS-DMA ring kernel, use the register-staged tiled kernel.
-// knob corr_path: 1 = literal per-element kernel, 2 = register-tiled kernel (measurement)
+// Kernel-selection override for cross-checks (PWC_DEBUG setting corr_path, read once):
+//   1: literal one-thread-per-output kernels only; 2: the register-tiled kernel (measurement)
 int force_generic() { return pwc::debug_knob("corr_path", 0); }
 
 }  // namespace
@@ -628,6 +626,9 @@ int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, int count
                                 int corr_multiply, int dtype, void* stream) {
   const char* fn = "pwc_warp_corr_forward_group";
   if (count < 0 || (count > 0 && !problems)) return fail(fn, "invalid problem list");
+  // every problem is checked as pwc_warp_corr_forward checks it BEFORE any launch, so a bad
+  // list never leaves work partly done (a NULL buffer would fault the pair kernel)
+  if (dtype < 0 || dtype > 2) return fail(fn, "unsupported dtype");
   for (int i = 0; i < count; ++i) {
     const pwc_warp_corr_problem& q = problems[i];
     int OC, Ho, Wo;
@@ -635,7 +636,10 @@ int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, int count
     if (!corr_shape(q.H, q.W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC,
                     &Ho, &Wo))
       return fail(fn, "invalid correlation parameters");
-    if ((size_t)q.B * q.C * q.H * q.W && !q.x2_warp) return fail(fn, "x2_warp is required");
+    if (Ho <= 0 || Wo <= 0) return fail(fn, "empty correlation output");
+    if ((size_t)q.B * q.C * q.H * q.W == 0) continue;
+    if (!q.in1 || !q.x2 || !q.flow || !q.out) return fail(fn, "null buffer");
+    if (!q.x2_warp) return fail(fn, "x2_warp is required");
   }
   // fused pairs first (in list order), then every problem left, one call each
   hipStream_t s = (hipStream_t)stream;
@@ -733,5 +737,6 @@ int pwc_corr_forward_group(const pwc_corr_problem* problems, int count, int pad_
                           max_displacement, stride1, stride2, corr_multiply, dtype, stream))
       return 0;
   }
+  pwc::g_ev_start = pwc::g_ev_stop = nullptr;  // one-shot, consumed or not
   return 1;
 }

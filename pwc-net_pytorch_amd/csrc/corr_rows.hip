@@ -483,9 +483,11 @@ hipError_t corr_forward_rows_pair(const void* a1, const void* a2, void* aout, in
       if (e != hipSuccess) return e;                                                          \
       attr = true;                                                                            \
     }                                                                                         \
-    hipLaunchKernelGGL((corr_fwd_rows_pair<float, RA, M1A, M2A, RB, M1B, M2B, NT>),           \
-                       dim3((unsigned)(nA + nB)), dim3(NT), lds, stream, A, Bq, (int)nA,      \
-                       current_epi());                                                        \
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                  \
+    take_launch_events(&ev0, &ev1); /* the one-shot timing hook times this launch */          \
+    hipExtLaunchKernelGGL((corr_fwd_rows_pair<float, RA, M1A, M2A, RB, M1B, M2B, NT>),        \
+                          dim3((unsigned)(nA + nB)), dim3(NT), lds, stream, ev0, ev1, 0, A,   \
+                          Bq, (int)nA, current_epi());                                        \
     return hipGetLastError();                                                                 \
   }
   // the variants the single launcher would pick (same first-match order: R 3 takes (2, 7)

@@ -148,6 +148,17 @@ def test_group_entry_host_checks():
     arr = (P * 1)(P(1, 1, 1, 1, 1, 1, 4, 6, 7))
     assert lib.pwc_warp_corr_forward_group(arr, 1, 9, 1, 9, 1, 0, 1, 0, None) == 0
     assert b"invalid correlation parameters" in lib.pwc_last_error()
+    # a NULL input in a pairable l0 + l1 list is rejected before the pair kernel launches
+    # (pwc_warp_corr_forward's own check, repeated up front)
+    l0 = P(1, 1, 1, 1, 1, 8, 192, 6, 7)
+    for bad in ((None, 1, 1, 1, 1), (1, None, 1, 1, 1), (1, 1, None, 1, 1), (1, 1, 1, 1, None)):
+        l1 = P(*bad, 8, 128, 12, 14)
+        arr = (P * 2)(l0, l1)
+        assert lib.pwc_warp_corr_forward_group(arr, 2, 9, 1, 9, 1, 2, 1, 0, None) == 0
+        assert b"null buffer" in lib.pwc_last_error()
+    arr = (P * 2)(l0, P(1, 1, 1, 1, 1, 8, 128, 12, 14))
+    assert lib.pwc_warp_corr_forward_group(arr, 2, 9, 1, 9, 1, 2, 1, 7, None) == 0
+    assert b"unsupported dtype" in lib.pwc_last_error()
     # an empty list is a no-op
     assert lib.pwc_warp_corr_forward_group(None, 0, 9, 1, 9, 1, 2, 1, 0, None) == 1
 
