@@ -13,8 +13,10 @@ it can run where /root/reference does not exist (the GPU box):
 * ``upsample_flow`` <- model.py:78 (F.upsample(flow, scale_factor=2, mode='bilinear') * 2,
                        torch-0.4 default align_corners=False)
 
-Pinned by tests/test_oracle_golden.py against the fixtures gen_golden.py produced from the
-reference's modules.py.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+Pinned directly by tests/test_torch_ref_golden.py against every fixture gen_golden.py produced
+from the reference's modules.py (cost_volume and warp forward + autograd backward, correlation
+through the CVL identities, upsample_flow + warp), and end to end by tests/test_net_harness.py
+(the reduced model.py Net).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
 (and bench.py's explicit ``--device cpu`` launcher rehearsal) use it; the product path
 (pwc-net_pytorch_amd/) never imports anything under oracle/.
 """
