@@ -1,5 +1,5 @@
 // colbench.hip -- standalone check + timing + phase census of the l4 column-item correlation
-// (csrc/corr_cols.hip), no torch.  B=8, C=32, 96x112 fp32 (config 2's l4): full compare with an
+// (tools/corr_cols.hip, a rejected prototype kept for the record), no torch.  B=8, C=32, 96x112 fp32 (config 2's l4): full compare with an
 // fp64 CPU restatement of correlation_cuda_kernel.cu:34-106, then per-launch hipExtLaunchKernel
 // event times over 6 rotating buffer sets (> the 256 MiB Infinity Cache) and per-workgroup
 // s_memrealtime phase stamps.
@@ -14,7 +14,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../pwc-net_pytorch_amd/csrc/corr_cols.hip"
+#include "corr_cols.hip"
 
 namespace pwc {
 hipEvent_t g_e0 = nullptr, g_e1 = nullptr;
@@ -36,14 +36,12 @@ int debug_knob(const char*, int def) { return def; }
     }                                                                                   \
   } while (0)
 
-// variants: cols::launch over other ring / loader geometries (measurement)
+// variants: cols::launch over other geometries (measurement)
 static hipError_t run_variant(int v, const float* a, const float* b, float* o, int B, int C,
                               int H, int W) {
   using namespace pwc::cols;
   switch (v) {
-    case 1: return launch<Geo<3, 14, 4, 8, 1, 2>>(a, b, o, B, C, H, W, W / 56, (float)C, 0);
-    case 2: return launch<Geo<3, 14, 4, 8, 2>>(a, b, o, B, C, H, W, W / 56, (float)C, 0);
-    case 3: return launch<Geo<3, 14, 4, 8, 2, 3>>(a, b, o, B, C, H, W, W / 56, (float)C, 0);
+    case 1: return launch<Geo<3, 14, 4, 4>>(a, b, o, B, C, H, W, W / 56, (float)C, 0);
     default: return pwc::corr_forward_cols(a, b, o, B, C, H, W, 0, (float)C, 0);
   }
 }
@@ -51,6 +49,7 @@ static hipError_t run_variant(int v, const float* a, const float* b, float* o, i
 int main(int argc, char** argv) {
   const int B = 8, C = 32, H = 96, W = 112, iters = argc > 1 ? std::atoi(argv[1]) : 200;
   const int abl = argc > 2 ? std::atoi(argv[2]) : 0, variant = argc > 3 ? std::atoi(argv[3]) : 0;
+  const int chk_abl = abl & 4;  // the check runs with the sync-only ablation bits
   const size_t nin = (size_t)B * C * H * W, nout = (size_t)B * 81 * H * W;
   const int NSET = 6;
   std::vector<float*> f1(NSET), f2(NSET), out(NSET);
@@ -78,17 +77,14 @@ int main(int argc, char** argv) {
   };
   // ---- correctness ----
   set_census(iters);
-  {
-    const int zero = 0;
-    CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::cols::g_abl), &zero, sizeof(int)));
-  }
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::cols::g_abl), &chk_abl, sizeof(int)));
   CK(run_variant(variant, f1[0], f2[0], out[0], B, C, H, W));
   CK(hipDeviceSynchronize());
   CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::cols::g_abl), &abl, sizeof(int)));
   std::vector<float> ho(nout);
   CK(hipMemcpy(ho.data(), out[0], nout * 4, hipMemcpyDeviceToHost));
   double maxerr = 0, maxref = 0;
-  long bad = 0;
+  long bad = 0, bad_tj[9] = {0}, bad_x[2] = {0}, bad_y[2] = {0};
   for (int n = 0; n < B; ++n)
     for (int tj = -4; tj <= 4; ++tj)
       for (int ti = -4; ti <= 4; ++ti)
@@ -103,10 +99,21 @@ int main(int argc, char** argv) {
             acc /= C;
             const float g = ho[(((size_t)n * 81 + (tj + 4) * 9 + ti + 4) * H + y) * W + x];
             const double e = std::fabs((double)g - acc);
-            if (!(e <= 1e-5)) ++bad;
+            if (!(e <= 1e-5)) {
+              if (bad < 6)
+                std::printf("bad n=%d tj=%d ti=%d y=%d x=%d got=%g ref=%g\n", n, tj, ti, y, x,
+                            (double)g, acc);
+              ++bad_tj[tj + 4];
+              ++bad_x[x / 56];
+              ++bad_y[y % 2];
+              ++bad;
+            }
             if (e > maxerr || e != e) maxerr = e != e ? 1e30 : std::max(maxerr, e);
             maxref = std::max(maxref, std::fabs(acc));
           }
+  std::printf("bad by tj: %ld %ld %ld %ld %ld %ld %ld %ld %ld; by item: %ld %ld; by parity %ld %ld\n",
+              bad_tj[0], bad_tj[1], bad_tj[2], bad_tj[3], bad_tj[4], bad_tj[5], bad_tj[6],
+              bad_tj[7], bad_tj[8], bad_x[0], bad_x[1], bad_y[0], bad_y[1]);
   std::printf("{\"check\": \"corr9 l4 B=8 vs fp64\", \"max_abs_err\": %.3e, \"max_abs_ref\": %.3f, \"bad\": %ld}\n",
               maxerr, maxref, bad);
 #ifndef PWC_COLS_M
@@ -143,15 +150,17 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(c.data(), cen, c.size() * 8, hipMemcpyDeviceToHost));
   // per slot: mean over workgroups of (stamp - the workgroup's wave-0 start), and the max over
   // workgroups of (stamp - the launch's earliest start)
-  const char* names[11] = {"start", "loader_entry", "loader_ready", "prologue_issued", "b0",
-                           "item0_loop", "item0_stored", "last_loop", "end", "last_landed",
-                           "compute_ready"};
-  double mean[11] = {0}, mx[11] = {0};
+  constexpr int NN = 14;
+  const char* names[NN] = {"start", "loader_loop", "grp1_start", "stage0_published", "stage0_seen",
+                           "item0_loop", "item0_stored", "item1_loop", "grp0_done",
+                           "last_published", "compute_ready", "grp1_done",
+                           "stage8_published", "stage8_issued"};
+  double mean[NN] = {0}, mx[NN] = {0};
   for (int i = 0; i < iters; ++i) {
     const unsigned long long* L = c.data() + (size_t)i * nblk * NSL;
     unsigned long long t0 = ~0ull;
     for (int b = 0; b < nblk; ++b) t0 = std::min(t0, L[b * NSL]);
-    for (int k = 0; k < 11; ++k) {
+    for (int k = 0; k < NN; ++k) {
       unsigned long long m = 0;
       for (int b = 0; b < nblk; ++b) {
         mean[k] += (double)(long long)(L[b * NSL + k] - L[b * NSL]) * 0.01 / nblk / iters;
@@ -164,7 +173,7 @@ int main(int argc, char** argv) {
   std::printf("{\"kernel\": \"corr_fwd_cols l4 B=8\", \"variant\": %d, \"abl\": %d, \"event_us_mean\": %.2f, "
               "\"event_us_min\": %.2f, \"frac_8TBs\": %.3f", variant, abl, mean_ev, sorted[0],
               bytes / (mean_ev * 1e-6) / 8e12);
-  for (int k = 1; k < 11; ++k) std::printf(", \"%s\": [%.2f, %.2f]", names[k], mean[k], mx[k]);
+  for (int k = 1; k < NN; ++k) std::printf(", \"%s\": [%.2f, %.2f]", names[k], mean[k], mx[k]);
   std::printf("}\n");
   return 0;
 }
