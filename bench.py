@@ -26,6 +26,13 @@ also makes the event-armed launch dearer), so graphs are comparis
 ``--timing graph-eager`` replays a per-set graph of l0..l3 and the l4 warp before the same
 event-armed launch; ``--timing graph-all`` captures the whole step in one graph, without
 kernel events (HIP refuses external event-record nodes in a capture).
+Order: the headline ``value`` runs the levels in DEPENDENCY order -- l0, l1, ..., l4, each
+level's warp before its correlation (l0 and l1 as one fused WarpCorrelation launch each), no
+launch batching work of different levels -- because in the network (model.py:72-113) level
+l+1's warp needs level l's flow.  The ``grouped`` object then times the same step with the
+independent synthetic levels batched into group launches (l0+l1 band pair, l2/l3/l4 warps,
+l2+l3 correlations): a labelled upper bound for batching across independent pairs, not the
+headline.
 Inputs rotate over enough buffer sets (> 2x the 256 MiB Infinity Cache) that each step reads
 them from HBM.  After timing, a replay self-check re-runs one step with every output poisoned
 (NaN) and compares all five levels bit for bit with a fresh eager computation, and a shard
@@ -115,19 +122,24 @@ def parse_args(argv=None):
                     help="cpu = launcher rehearsal over gloo with a torch-CPU stand-in op")
     ap.add_argument("--fused-levels", default="0,1",
                     help="levels run as one fused warp->correlation launch (WarpCorrelation)")
+    ap.add_argument("--grouped-mode", default="on", choices=["on", "off"],
+                    help="after the headline (dependency order: one level after the other, "
+                         "as model.py:72-113 runs them), time the same step with independent "
+                         "levels batched into group launches (--group / --corr-group / "
+                         "--warp-group below) and report it as the separate 'grouped' object")
     ap.add_argument("--group", default="on", choices=["on", "off"],
-                    help="issue the fused levels as one group (pwc_warp_corr_forward_group: "
-                         "the bench's levels take independent inputs, so l0 + l1 share one "
-                         "launch); off = one call per level")
+                    help="grouped mode: issue the fused levels as one group "
+                         "(pwc_warp_corr_forward_group: the bench's levels take independent "
+                         "inputs, so l0 + l1 share one launch); off = one call per level")
     ap.add_argument("--corr-group", default="on", choices=["on", "off"],
-                    help="the unfused levels' correlations below l4 (l2, l3) as one "
+                    help="grouped mode: the unfused levels' correlations below l4 (l2, l3) as one "
                          "pwc_corr_forward_group launch (independent inputs); off = one call "
                          "per level")
     ap.add_argument("--group-order", default="desc", choices=["asc", "desc"],
                     help="problem order inside the warp / correlation groups: asc = l2 first, "
                          "desc = the largest level's workgroups dispatched first")
     ap.add_argument("--warp-group", default="on", choices=["on", "off"],
-                    help="the unfused levels' warps (l2, l3, l4) as one pwc_warp_forward_group "
+                    help="grouped mode: the unfused levels' warps (l2, l3, l4) as one pwc_warp_forward_group "
                          "launch ahead of their correlations (independent inputs); off = one "
                          "warp call per level")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02l_l4corr_pmc.json"),
@@ -737,7 +749,7 @@ def main(argv=None):
         torch.cuda.set_device(dev)
         if world > 1:
             dist.init_process_group("nccl", device_id=dev)
-    from pwcnet_amd.shard import max_over_ranks
+    from pwcnet_amd.shard import all_ranks, max_over_ranks
 
     dtype = torch.float32 if args.dtype == "fp32" else torch.float16
     esz = 4 if dtype == torch.float32 else 2
@@ -746,34 +758,50 @@ def main(argv=None):
     fused = {int(v) for v in args.fused_levels.split(",") if v.strip()}
     bcast = broadcast_weights(dev) if world > 1 else None
 
+    gpass = None
     if cpu:
         pass_ = CpuStandinPass()
         sets = [checked_set(list(range(rank * B, rank * B + B)), shapes, dev, dtype)]
         nsets = 1
     else:
-        pass_ = HipPass(dev, dtype, fused, group=args.group == "on",
-                        warp_group=args.warp_group == "on",
-                        corr_group=args.corr_group == "on",
-                        group_desc=args.group_order == "desc")
+        # headline: dependency order -- level after level, each level's warp before its
+        # correlation, nothing batched across levels (model.py:72-113 needs level l's flow
+        # before level l+1's warp)
+        pass_ = HipPass(dev, dtype, fused)
+        if args.grouped_mode == "on":
+            gpass = HipPass(dev, dtype, fused, group=args.group == "on",
+                            warp_group=args.warp_group == "on",
+                            corr_group=args.corr_group == "on",
+                            group_desc=args.group_order == "desc")
+            if not (gpass.grouped_levels(shapes) or gpass.warp_levels(shapes)):
+                gpass = None
         per_set = sum((2 * C * h * w + 2 * h * w + 81 * h * w + C * h * w) * B * esz
                       for C, h, w in shapes)
         nsets = args.sets or max(2, int(np.ceil(2 * 256 * 2 ** 20 / per_set)))
         gen = torch.Generator(device=dev).manual_seed(1234 + rank)
         sets = [random_set(shapes, B, dev, dtype, gen) for _ in range(nsets)]
 
-    graphs, preps = [], []
+    graphs, preps, gpreps = [], [], []
     timing = "cpu" if cpu else ("eager" if args.no_graph else args.timing)
     if not cpu:
         for s in sets:
             pass_.bind(s)
         for s in sets:  # first calls (kernel attributes) outside any capture
             pass_.full(s)
+            if gpass is not None:
+                gpass.full(s)
         torch.cuda.synchronize(dev)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
-        for a, b in evs:  # materialise the hipEvent_t handles (torch creates them lazily)
-            a.record()
-            b.record()
+
+        def make_events():
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.steps)]
+            for a, b in evs:  # materialise the hipEvent_t handles (torch creates them lazily)
+                a.record()
+                b.record()
+            return evs
+
+        evs = make_events()
+        gevs = make_events() if gpass is not None else None
         torch.cuda.synchronize(dev)
         if timing == "graph-all":
             # comparison mode: one hipGraph per buffer set with the WHOLE step (l4 correlation
@@ -798,6 +826,8 @@ def main(argv=None):
             # eager: every launch a direct C-ABI call on pre-built ctypes arguments (on ROCm
             # this step runs faster as plain launches than as graph replays)
             preps = [pass_.prepare(s) for s in sets]
+        if gpass is not None:
+            gpreps = [gpass.prepare(s) for s in sets]
         torch.cuda.synchronize(dev)
 
     def step(i, ev=None):
@@ -817,41 +847,73 @@ def main(argv=None):
             pass_.pre(s)
         pass_.corr_l4(s, ev)
 
+    def gstep(i, ev=None):
+        gpass.step_prepared(gpreps[i % nsets], ev)
+
     def sync():
         if not cpu:
             torch.cuda.synchronize(dev)
 
-    for i in range(args.warmup):
-        step(i)
-    sync()
-    if world > 1:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, None if cpu else evs[i])
-    issued = time.perf_counter() - t0  # host time to issue the steps (GPU-bound if << elapsed)
-    sync()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, device=dev)  # MAX over ranks (no-op at N=1)
+    def timed(stepf, events):
+        """W untimed steps, then K timed ones between barrier + synchronize on both sides;
+        returns (MAX over ranks of the elapsed time, this rank's issue time, every rank's
+        elapsed time)."""
+        for i in range(args.warmup):
+            stepf(i)
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            stepf(i, None if events is None else events[i])
+        issued = time.perf_counter() - t0  # host time to issue the steps (GPU-bound if << elapsed)
+        sync()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        return max_over_ranks(el, device=dev), issued, all_ranks(el, device=dev)
 
-    # ---- replay self-check: poison one set's outputs, run one step, compare with fresh ----
-    k = (args.steps - 1) % nsets
-    s = sets[k]
-    for lv in s:
-        lv["corr"].fill_(float("nan"))
-    step(k)
-    sync()
-    ref = pass_.fresh(s)
-    replay_diff = [_diff(lv["corr"], r) for lv, r in zip(s, ref)]
-    replay_ok = all(d <= 1e-5 for d in replay_diff)
+    def self_check(stepf, p):
+        """Poison one set's outputs, run one step, compare every level with a fresh eager
+        computation (a skipped kernel leaves the NaN poison)."""
+        k = (args.steps - 1) % nsets
+        s = sets[k]
+        for lv in s:
+            lv["corr"].fill_(float("nan"))
+        stepf(k)
+        sync()
+        ref = p.fresh(s)
+        diff = [_diff(lv["corr"], r) for lv, r in zip(s, ref)]
+        ok = all(d <= 1e-5 for d in diff)
+        if world > 1:
+            flag = torch.tensor([int(ok)], device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = bool(flag.item())
+        return ok, diff
+
+    elapsed, issued, per_rank = timed(step, None if cpu else evs)
+    replay_ok, replay_diff = self_check(step, pass_)
+    grouped = None
+    if gpass is not None:
+        g_el, g_issued, g_per_rank = timed(gstep, gevs)
+        g_ok, g_diff = self_check(gstep, gpass)
+        g_kern = float(np.mean([a.elapsed_time(b) for a, b in gevs]))
+        grouped = {
+            "mode": "grouped (NOT the headline: independent levels batched into group launches, "
+                    "which the network's level-to-level flow dependency does not allow)",
+            "value": round(B * args.steps * world / g_el, 2),
+            "ms_per_step": round(g_el / args.steps * 1e3, 5),
+            "host_issue_ms_per_step": round(g_issued / args.steps * 1e3, 5),
+            "per_rank_ms_per_step": [round(v / args.steps * 1e3, 5) for v in g_per_rank],
+            "grouped_levels": gpass.grouped_levels(shapes),
+            "warp_grouped_levels": gpass.warp_levels(shapes),
+            "corr_grouped_levels": gpass.corr_levels(shapes),
+            "l4_corr_us": round(g_kern * 1e3, 3),
+            "replay": g_ok, "replay_max_rel_diff": g_diff,
+        }
+        replay_ok = replay_ok and g_ok
     shards = shard_check(pass_, shapes, B, world, rank, dev, dtype)
-    if world > 1:
-        flag = torch.tensor([int(replay_ok)], device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        replay_ok = bool(flag.item())
 
     C4, h4, w4 = shapes[-1]
     pairs = B * args.steps * world
@@ -876,6 +938,7 @@ def main(argv=None):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "per_rank_ms_per_step": [round(v / args.steps * 1e3, 5) for v in per_rank],
         "host_issue_ms_per_step": round(issued / args.steps * 1e3, 5),
         "higher_is_better": True,
         "scaling": "weak",
@@ -893,9 +956,7 @@ def main(argv=None):
             "parallelism": f"dp{world} (batch-sharded replicas, no data-path collective)",
             "buffer_sets": nsets,
             "fused_levels": sorted(fused),
-            "grouped_levels": (pass_.grouped_levels(shapes) if not cpu else []),
-            "warp_grouped_levels": (pass_.warp_levels(shapes) if not cpu else []),
-            "corr_grouped_levels": (pass_.corr_levels(shapes) if not cpu else []),
+            "order": "dependency (level after level; warp before correlation within a level)",
             "graph": bool(graphs),
             "timing": timing,
             "device": "cpu (launcher rehearsal: torch-CPU stand-in, not the product path)"
@@ -904,6 +965,8 @@ def main(argv=None):
         "checks": {"replay": replay_ok, "replay_max_rel_diff": replay_diff, "shards": shards,
                    "weights_broadcast": bcast},
     }
+    if grouped is not None:
+        result["grouped"] = grouped
     if not cpu and timing != "graph-all":
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
         bytes_launch = corr_bytes_per_pair(C4, h4, w4, esz) * B

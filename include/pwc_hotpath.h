@@ -58,7 +58,8 @@ extern "C" {
 
 /* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
  * 4: fused warp -> correlation, 5: fused flow upsample -> warp, corr into a slice,
- * 6: pwc_set_debug, 7: grouped warp / warp -> correlation launches). */
+ * 6: pwc_set_debug, 7: grouped warp / warp -> correlation launches, 8: one-launch warp
+ * backward with a workspace). */
 PWC_API int pwc_abi_version(void);
 
 /* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
@@ -167,6 +168,17 @@ PWC_API int pwc_warp_forward_group(const pwc_warp_problem* problems, int count, 
  * added with fp32 atomics.  fp32 only. */
 PWC_API int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, void* grad_x,
                       void* grad_flow, int B, int C, int H, int W, int dtype, void* stream);
+/* Same result with a caller-owned device workspace of at least
+ * pwc_warp_backward_workspace_size() bytes (no initialisation needed).  On wide images
+ * (W >= 96: the l4 level) grad_x and grad_flow come from one tile kernel -- per 16x16 tile of
+ * grad_x its output pixels' lists (fixed order) with x and grad_out streamed through LDS --
+ * plus a small kernel that adds the channel groups' grad_flow partials (fixed order) and the
+ * rare corners beyond the tiles' 8-pixel margins (fp32 atomics).  Other sizes, or a NULL /
+ * short workspace, run pwc_warp_backward's kernels.  fp32 only. */
+PWC_API size_t pwc_warp_backward_workspace_size(int B, int C, int H, int W, int dtype);
+PWC_API int pwc_warp_backward_ws(const void* x, const void* flow, const void* grad_out,
+                                 void* grad_x, void* grad_flow, int B, int C, int H, int W,
+                                 int dtype, void* workspace, size_t workspace_bytes, void* stream);
 
 /* model.py:78 + :80 in one launch: flow_up = bilinear x2 upsample of flow_coarse
  * ([B][2][H/2][W/2], ATen upsample_bilinear2d with align_corners=False -- torch 0.4's default)

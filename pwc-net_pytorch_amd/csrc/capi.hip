@@ -29,6 +29,9 @@ template <typename T>
 hipError_t warp_forward_group_t(const WarpProblem*, int, hipStream_t);
 hipError_t warp_backward_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                              int, hipStream_t);
+size_t warp_backward_workspace_size(int B, int C, int H, int W);
+hipError_t warp_backward_tiles_f32(const void*, const void*, const void*, void*, void*, int, int,
+                                   int, int, void*, size_t, hipStream_t);
 template <typename T>
 hipError_t upsample_warp_forward_t(const void*, const void*, void*, void*, int, int, int, int,
                                    hipStream_t);
@@ -143,7 +146,7 @@ int force_generic() { return pwc::debug_knob("corr_path", 0); }
 
 extern "C" {
 
-int pwc_abi_version(void) { return 7; }
+int pwc_abi_version(void) { return 8; }
 
 int pwc_set_debug(const char* spec) {
   pwc::debug_spec() = spec ? spec : "";
@@ -507,6 +510,28 @@ int pwc_warp_backward(const void* x, const void* flow, const void* grad_out, voi
   if (dtype != PWC_DTYPE_F32) return fail(fn, "backward is fp32 only");
   if ((size_t)B * H * W && (!x || !flow || !grad_out || !grad_x || !grad_flow))
     return fail(fn, "null buffer");
+  return check_launch(fn, pwc::warp_backward_f32(x, flow, grad_out, grad_x, grad_flow, B, C, H,
+                                                 W, (hipStream_t)stream));
+}
+
+size_t pwc_warp_backward_workspace_size(int B, int C, int H, int W, int dtype) {
+  if (!dims_ok(B, C, H, W) || dtype != PWC_DTYPE_F32) return 0;
+  return pwc::warp_backward_workspace_size(B, C, H, W);
+}
+
+int pwc_warp_backward_ws(const void* x, const void* flow, const void* grad_out, void* grad_x,
+                         void* grad_flow, int B, int C, int H, int W, int dtype, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  const char* fn = "pwc_warp_backward_ws";
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (dtype != PWC_DTYPE_F32) return fail(fn, "backward is fp32 only");
+  if ((size_t)B * H * W && (!x || !flow || !grad_out || !grad_x || !grad_flow))
+    return fail(fn, "null buffer");
+  if ((size_t)B * H * W == 0) return 1;
+  const hipError_t e =
+      pwc::warp_backward_tiles_f32(x, flow, grad_out, grad_x, grad_flow, B, C, H, W, workspace,
+                                   workspace_bytes, (hipStream_t)stream);
+  if (e != hipErrorNotSupported) return check_launch(fn, e);
   return check_launch(fn, pwc::warp_backward_f32(x, flow, grad_out, grad_x, grad_flow, B, C, H,
                                                  W, (hipStream_t)stream));
 }

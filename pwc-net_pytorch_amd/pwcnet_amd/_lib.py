@@ -64,6 +64,8 @@ SYMBOLS = {
     "pwc_cost_volume_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 6 + [_P]),
     "pwc_warp_forward": (_I, [_P, _P, _P] + [_I] * 5 + [_P]),
     "pwc_warp_backward": (_I, [_P, _P, _P, _P, _P] + [_I] * 5 + [_P]),
+    "pwc_warp_backward_workspace_size": (_Z, [_I] * 5),
+    "pwc_warp_backward_ws": (_I, [_P, _P, _P, _P, _P] + [_I] * 5 + [_P, _Z, _P]),
     "pwc_warp_corr_workspace_size": (_Z, [_I] * 11),
     "pwc_warp_corr_forward": (_I, [_P] * 5 + [_I] * 11 + [_P, _Z, _P]),
     "pwc_warp_corr_forward_group": (_I, [ctypes.POINTER(WarpCorrProblem)] + [_I] * 8 + [_P]),
@@ -75,7 +77,7 @@ SYMBOLS = {
     "pwc_corr_forward_into": (_I, [_P, _P, _P, ctypes.c_longlong, ctypes.c_float] + [_I] * 11
                               + [_P, _Z, _P]),
 }
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lock = threading.Lock()
 _lib = None

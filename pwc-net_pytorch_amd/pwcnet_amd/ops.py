@@ -347,9 +347,13 @@ def warp_backward(x, flow, grad_output):
     gf = torch.empty_like(flow)
     if gf.numel() == 0:
         return gx, gf
-    _lib.check(_lib.load().pwc_warp_backward(_ptr(x), _ptr(flow), _ptr(grad_output), _ptr(gx),
-                                             _ptr(gf), B, C, H, W, 0, _stream(x.device)),
+    lib = _lib.load()
+    nws = lib.pwc_warp_backward_workspace_size(B, C, H, W, 0)
+    ws, wsp = _workspace(nws, x.device)
+    _lib.check(lib.pwc_warp_backward_ws(_ptr(x), _ptr(flow), _ptr(grad_output), _ptr(gx),
+                                        _ptr(gf), B, C, H, W, 0, wsp, nws, _stream(x.device)),
                "WarpingLayer_backward")
+    del ws
     return gx, gf
 
 

@@ -7,7 +7,8 @@ cross-GPU traffic.  The only collectives are outside the data path:
 * ``broadcast_module`` -- one RCCL broadcast of a model's parameters from rank 0 over xGMI
   (the Net harness's 20.5 MB of conv weights; the hot-path layers have no parameters),
 * ``gather_to`` -- optional gather of per-rank outputs (e.g. final flows) to one rank,
-* ``max_over_ranks`` -- the benchmark's barrier-bounded timing (MAX of per-rank elapsed).
+* ``max_over_ranks`` -- the benchmark's barrier-bounded timing (MAX of per-rank elapsed),
+* ``all_ranks`` -- every rank's value of a scalar (the benchmark's per-rank timings).
 
 Everything here is backend-agnostic torch.distributed: "nccl" (= RCCL on ROCm) on GPUs,
 "gloo" for the CPU tests.
@@ -70,3 +71,13 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_ranks(value: float, device=None) -> list:
+    """[value of rank 0, value of rank 1, ...] on every rank (all_gather of one float64)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [value]
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [float(p.item()) for p in parts]

@@ -207,6 +207,51 @@ def test_warp_vs_oracle(shape):
     np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
 
 
+@pytest.mark.parametrize("scale", [0.0, 2.0, 7.5, 25.0])
+@pytest.mark.parametrize("shape", [(8, 32, 96, 112), (8, 64, 48, 56), (2, 96, 24, 28),
+                                   (2, 128, 12, 14), (2, 192, 6, 7), (1, 13, 37, 70),
+                                   (1, 3, 9, 2), (3, 5, 17, 33)])
+def test_warp_backward_one_launch_vs_oracle(shape, scale):
+    """pwc_warp_backward_ws (16x16 grad_x tiles with 8-px margins and channel groups, then a
+    small kernel for the groups' grad_flow partials and the far corners) against the float64
+    oracle: zero flow, in-margin, around the margin and far beyond it; ragged tiles, W % 4 != 0,
+    a 2-pixel-wide image; and against the multi-kernel path (PWC_DEBUG warp_bwd_tiles=0)."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import warp_backward
+    B, C, H, W = shape
+    rng = np.random.default_rng(int(scale * 4) + 7 * H + W)
+    x = _rand(rng, B, C, H, W)
+    f = (rng.standard_normal((B, 2, H, W)) * scale).astype(np.float32)
+    g = _rand(rng, B, C, H, W)
+    _lib.set_debug("warp_bwd_tiles=2")  # the one-launch path at every size
+    try:
+        gx, gf = warp_backward(_t(x), _t(f), _t(g))
+        _lib.set_debug("warp_bwd_tiles=0")
+        gx0, gf0 = warp_backward(_t(x), _t(f), _t(g))
+    finally:
+        _lib.set_debug("")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(gx), _np(gx0), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_np(gf), _np(gf0), rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)),
+                               equal_nan=True)
+    if x.size <= 2 * 96 * 24 * 28:
+        rx, rf = O.warp_backward(x, f, g)
+        np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)),
+                                   equal_nan=True)
+
+
+def test_warp_backward_one_launch_repeatable():
+    """No far corners -> no atomics: two calls agree bit for bit (fixed list and group order)."""
+    from pwcnet_amd.ops import warp_backward
+    rng = np.random.default_rng(3)
+    x, g = _rand(rng, 4, 32, 96, 112), _rand(rng, 4, 32, 96, 112)
+    f = (rng.standard_normal((4, 2, 96, 112)) * 2).clip(-6, 6).astype(np.float32)
+    a = warp_backward(_t(x), _t(f), _t(g))
+    b = warp_backward(_t(x), _t(f), _t(g))
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
 @pytest.mark.parametrize("scale", [0.0, 6.0, 25.0])
 def test_warp_backward_tiles_and_outliers(scale):
     # grad_x of the LDS-binned kernel (tiles of 8x32, candidate margin 8) + the corners left

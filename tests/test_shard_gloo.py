@@ -113,6 +113,10 @@ def test_bench_launcher_two_ranks_cpu_rehearsal():
     assert d["checks"]["shards"] == {"pairs": 4, "ranks": 2, "ok": True, "bad_ranks": []}
     assert d["checks"]["weights_broadcast"]["ok"] is True
     assert d["checks"]["weights_broadcast"]["bytes"] == 20475776
+    assert d["checks"]["weights_broadcast"]["seconds"] >= 0
+    # every rank's own step time, the headline being their MAX
+    assert len(d["per_rank_ms_per_step"]) == 2
+    assert abs(max(d["per_rank_ms_per_step"]) - d["ms_per_step"]) <= 1e-4 * d["ms_per_step"] + 1e-4
 
 
 def test_bench_rejects_gpus_world_mismatch():
