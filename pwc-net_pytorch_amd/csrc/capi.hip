@@ -709,12 +709,14 @@ int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, int count
 // A problem the row-band kernel takes in a single call: model.py:24's configuration in fp32,
 // rows too narrow for the stream kernel (W < 64), too many for the band kernel ((H+1)/2 > 6),
 // 16-B aligned buffers (corr_fwd.hip's dispatch order: stream, band, rows).
+// Two problems share a row-band launch only when the single-call dispatch would run each on
+// the row-band kernel (the same predicate corr_forward_t dispatches by): then the paired result
+// equals the single calls' bit for bit.
 static bool rows_pairable(const pwc_corr_problem& q, int pad, int k, int md, int s1, int s2,
                           int dtype) {
-  return dtype == PWC_DTYPE_F32 && k == 1 && s1 == 1 && s2 == 2 && pad == md &&
-         (md == 8 || md == 9) && force_generic() == 0 && q.W < 64 && (q.H + 1) / 2 > 6 &&
-         (size_t)q.B * q.C * q.H * q.W > 0 && (uintptr_t)q.in1 % 16 == 0 &&
-         (uintptr_t)q.in2 % 16 == 0 && (uintptr_t)q.out % 16 == 0;
+  return dtype == PWC_DTYPE_F32 && force_generic() == 0 && (size_t)q.B * q.C * q.H * q.W > 0 &&
+         pwc::corr_forward_path(q.in1, q.in2, q.out, q.B, q.C, q.H, q.W, pad, k, md, s1, s2,
+                                pwc::kRaster, 0) == pwc::kPathRows;
 }
 
 int pwc_corr_forward_group(const pwc_corr_problem* problems, int count, int pad_size,

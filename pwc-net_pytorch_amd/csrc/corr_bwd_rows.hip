@@ -295,8 +295,8 @@ __global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__
 
 }  // namespace bwdrows
 
-// PWC_BWD_ROWS=0 disables the kernel; PWC_BWD_CFG="R,CT" forces a band height and channels per
-// item (measurement).
+// Measurement knobs (PWC_DEBUG / pwc_set_debug): bwd_rows=0 disables the kernel; bwd_r, bwd_ct
+// force a band height and channels per item; bwd_slices the channel slices.
 hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* gout, void* g1,
                                   void* g2, int B, int C, int H, int W, float divisor,
                                   hipStream_t stream) {

@@ -500,12 +500,12 @@ size_t corr_workspace_bytes(int B, int OC, int Ho, int Wo) {
   return k > 1 ? (size_t)k * B * OC * Ho * Wo * sizeof(float) : 0;
 }
 
-// PWC_CORR_PT=0 disables the parity-tile kernel (measurement of the older paths).
+// knob corr_pt=0 disables the parity-tile kernel (measurement of the older paths).
 static bool pt_disabled() { return debug_knob("corr_pt", 1) == 0; }
 
 // The band kernel of warp_corr.hip (without the warp) serves model.py:24's correlation at the
 // smallest levels (parity half of <= 6 rows: l0, l1 at 384x448; measured 6.8 / 7.8 us against
-// 11.0 / 13.4 us for corr_small + its reduce).  PWC_CORR_BAND=0 disables it, =1 forces it at
+// 11.0 / 13.4 us for corr_small + its reduce).  Knob corr_band=0 disables it, =2 forces it at
 // every size (measurement).
 static int band_mode() { return debug_knob("corr_band", 1); }
 
@@ -518,10 +518,34 @@ hipError_t corr_forward_rows(const void*, const void*, void*, int, int, int, int
 // corr_stream.hip: full-width row bands + loader wave (the l4-sized grids; it decides).
 hipError_t corr_forward_stream(const void*, const void*, void*, int, int, int, int, int, int,
                                int, float, hipStream_t);
+bool corr_stream_accepts(const void*, const void*, const void*, int, int, int, int, int, int);
+bool corr_rows_accepts(int, int, int, int, int);
+bool warp_corr_band_accepts(int, int, int, int, int);
+
+// The first stages of corr_forward_t's dispatch as one predicate: which of the stream, band and
+// row-band kernels serves a problem (kPathOther: a later stage).  corr_forward_t launches in this
+// order, and the group entry (capi.hip) pairs two problems in one row-band launch only when both
+// would take the row-band kernel alone -- so a grouped result equals the single call's.
+int corr_forward_path(const void* in1, const void* in2, const void* out, int B, int C, int H,
+                      int W, int pad, int k, int md, int s1, int s2, int layout, int dtype) {
+  const bool half = dtype == 1;
+  if (k != 1 || s1 != 1) return kPathOther;
+  if ((dtype == 0 || half) && pad == md && md / s2 == 4 && (s2 == 1 || s2 == 2) &&
+      corr_stream_accepts(in1, in2, out, B, C, H, W, s2, half ? 1 : 0))
+    return kPathStream;
+  const bool c9 = layout == kRaster && s2 == 2 && pad == md && (md == 8 || md == 9);
+  if (c9 && dtype == 0 && (band_mode() == 2 || (band_mode() == 1 && (H + 1) / 2 <= 6)) &&
+      warp_corr_band_accepts(B, C, H, W, 0))
+    return kPathBand;
+  if (c9 && (dtype == 0 || half) && (uintptr_t)in1 % 16 == 0 && (uintptr_t)in2 % 16 == 0 &&
+      (uintptr_t)out % 16 == 0 && corr_rows_accepts(B, C, H, W, half ? 1 : 0))
+    return kPathRows;
+  return kPathOther;
+}
 
 // corr_rows.hip (row bands over full rows) serves l3-sized grids (it decides; PWC_ROWS).
 
-// PWC_CORR_GRP=0 disables the coarse-level kernel (measurement of the split path only).
+// knob corr_grp=0 disables the coarse-level kernel (measurement of the split path only).
 static bool grp_disabled() { return debug_knob("corr_grp", 1) == 0; }
 
 // `workspace` (>= corr_workspace_bytes) enables channel splitting for grids too small to fill
@@ -540,26 +564,17 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
   // parity-tile and ring kernels only; every other path declines before launching
   const bool epi_def = epi_is_default(current_epi());
   constexpr bool kHalf = std::is_same<T, __half>::value;
-  if (force_generic == 0 && k == 1 && s1 == 1 && (sizeof(T) == 4 || kHalf) && pad == md &&
-      dr == 4 && (s2 == 1 || s2 == 2)) {
-    const hipError_t e = corr_forward_stream(in1, in2, out, B, C, H, W, s2, kHalf ? 1 : 0,
-                                             layout, divisor, stream);
-    if (e != hipErrorNotSupported) return e;
-  }
-  if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4 && layout == kRaster &&
-      s2 == 2 && pad == md && (md == 8 || md == 9) &&
-      (band_mode() == 2 || (band_mode() == 1 && (H + 1) / 2 <= 6))) {
-    const hipError_t e =
-        warp_corr_band_f32(in1, in2, nullptr, nullptr, out, B, C, H, W, divisor, 0, stream);
-    if (e != hipErrorNotSupported) return e;
-  }
-  if (force_generic == 0 && k == 1 && s1 == 1 && (sizeof(T) == 4 || kHalf) &&
-      layout == kRaster && s2 == 2 && pad == md && (md == 8 || md == 9) &&
-      (uintptr_t)in1 % 16 == 0 && (uintptr_t)in2 % 16 == 0 && (uintptr_t)out % 16 == 0) {
-    const hipError_t e =
-        corr_forward_rows(in1, in2, out, B, C, H, W, divisor, kHalf ? 1 : 0, stream);
-    if (e != hipErrorNotSupported) return e;
-  }
+  const int path = force_generic == 0 && (sizeof(T) == 4 || kHalf)
+                       ? corr_forward_path(in1, in2, out, B, C, H, W, pad, k, md, s1, s2, layout,
+                                           kHalf ? 1 : 0)
+                       : kPathOther;
+  if (path == kPathStream)
+    return corr_forward_stream(in1, in2, out, B, C, H, W, s2, kHalf ? 1 : 0, layout, divisor,
+                               stream);
+  if (path == kPathBand)
+    return warp_corr_band_f32(in1, in2, nullptr, nullptr, out, B, C, H, W, divisor, 0, stream);
+  if (path == kPathRows)
+    return corr_forward_rows(in1, in2, out, B, C, H, W, divisor, kHalf ? 1 : 0, stream);
   if (force_generic == 0 && k == 1 && s1 == 1 && sizeof(T) == 4) {
     // stride-2 displacements with 16-B aligned rows (l2..l4 of PWC-Net): parity tiles
     // (corr_pt.hip), channel groups chosen by grid size

@@ -337,25 +337,12 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int C, int
   return hipGetLastError();
 }
 
-// Configurations (JG, K, CC, NS, dword DMA); PWC_GRP_CFG=<letter> forces one for measurement.
-using GA = GrpTile<1, 8, 1, 3, false>;  // 72 KiB ring, 8 waves
-using GB = GrpTile<1, 4, 2, 3, false>;  // 72 KiB, 4 waves
+// Configurations (JG, K, CC, NS, dword DMA): round 2 measured eight ring shapes (A..H); the two
+// the dispatcher picks stayed in the library.
 using GC = GrpTile<1, 8, 1, 2, false>;  // 48 KiB, 8 waves
 using GD = GrpTile<3, 2, 3, 3, false>;  // 6 waves, 3 tj rows per workgroup, 72 KiB
-using GE = GrpTile<1, 16, 1, 2, false>; // 16 waves, 96 KiB
-using GF = GrpTile<1, 8, 1, 6, false>;  // 144 KiB: 4 stages in flight, 1 workgroup/CU
-using GG = GrpTile<1, 4, 2, 5, false>;  // 120 KiB
-using GH = GrpTile<3, 2, 3, 6, false>;  // 144 KiB
-using GAd = GrpTile<1, 8, 1, 3, true>;
-using GBd = GrpTile<1, 4, 2, 3, true>;
 using GCd = GrpTile<1, 8, 1, 2, true>;
 using GDd = GrpTile<3, 2, 3, 3, true>;
-using GEd = GrpTile<1, 16, 1, 2, true>;
-using GFd = GrpTile<1, 8, 1, 6, true>;
-using GGd = GrpTile<1, 4, 2, 4, true>;
-using GHd = GrpTile<3, 2, 3, 6, true>;
-
-int grp_cfg() { return debug_knob("grp_cfg", -1); }  // 0..7 = A..H (measurement)
 
 }  // namespace grp
 
@@ -368,25 +355,15 @@ hipError_t corr_forward_grp_f32(const void* in1, const void* in2, void* out, int
   if ((size_t)C * H * W * 4 >= 0x7ffffff0ull) return hipErrorNotSupported;
   const bool dw = !(W % 4 == 0 && off % 4 == 0 && (uintptr_t)in1 % 16 == 0 &&
                     (uintptr_t)in2 % 16 == 0);
-  int cfg = grp_cfg();
-  if (cfg < 0) {
-    // default: one tj row per workgroup (9 workgroups per tile) and 8 channel groups in a
-    // 2-deep ring (3 workgroups per CU); 3 rows per workgroup once that fills the chip
-    const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
-    cfg = tiles * 3 >= 256 ? 3 : 2;  // measured: D at 48x56 (B 8), C at 24x28
-  }
+  // one tj row per workgroup (9 workgroups per tile) and 8 channel groups in a 2-deep ring (3
+  // workgroups per CU); 3 rows per workgroup once that fills the chip (measured: D at 48x56
+  // (B 8), C at 24x28)
+  const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
+  const bool d = tiles * 3 >= 256;
 #define PWC_GRP_LAUNCH(T) \
   launch<T>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream)
-  switch (cfg) {
-    case 1: return dw ? PWC_GRP_LAUNCH(GBd) : PWC_GRP_LAUNCH(GB);
-    case 2: return dw ? PWC_GRP_LAUNCH(GCd) : PWC_GRP_LAUNCH(GC);
-    case 3: return dw ? PWC_GRP_LAUNCH(GDd) : PWC_GRP_LAUNCH(GD);
-    case 4: return dw ? PWC_GRP_LAUNCH(GEd) : PWC_GRP_LAUNCH(GE);
-    case 5: return dw ? PWC_GRP_LAUNCH(GFd) : PWC_GRP_LAUNCH(GF);
-    case 6: return dw ? PWC_GRP_LAUNCH(GGd) : PWC_GRP_LAUNCH(GG);
-    case 7: return dw ? PWC_GRP_LAUNCH(GHd) : PWC_GRP_LAUNCH(GH);
-    default: return dw ? PWC_GRP_LAUNCH(GAd) : PWC_GRP_LAUNCH(GA);
-  }
+  if (d) return dw ? PWC_GRP_LAUNCH(GDd) : PWC_GRP_LAUNCH(GD);
+  return dw ? PWC_GRP_LAUNCH(GCd) : PWC_GRP_LAUNCH(GC);
 #undef PWC_GRP_LAUNCH
 }
 

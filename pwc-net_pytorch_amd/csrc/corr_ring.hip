@@ -361,568 +361,12 @@ __global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ring(
 }
 
 // ------------------------------------------------------------------------------------
-// Software-pipelined ring kernel (same tile, waves, DMA ring and LDS image as corr_fwd_ring).
-// The per-channel "6 reads, wait for all, 36 FMAs" of corr_fwd_ring leaves every wave idle for
-// an LDS round trip per channel, and at <= 4.5 waves per SIMD the other waves do not cover it
-// (measured: VALU and the LDS array each < 25 % busy).  Here a lane's reads for channel c+1
-// are issued into the registers channel c has finished with, in the order channel c+1 needs
-// them, and each displacement ti waits only for its own quads (counted lgkmcnt):
-//   f1 quad A and window quads Q0..Q4 of channel c+1 go out after ti = 1, 3, 5, 7, 8 of
-//   channel c, so 4 reads stay in flight under the FMAs (A is double-buffered: 4 VGPRs).
-// The stage barrier moves into the last channel of a stage (after ti = 1, before the first
-// read of the next stage), so the ring keeps NS-2 stages in flight instead of NS-1.  Stages
-// are unrolled NS at a time so every LDS offset (slot, channel) is an instruction immediate.
+// configuration: three workgroups per 16x16 tile (3 tj rows each, 24-row f2 tiles), 2 channels
+// per stage, 5-deep ring (4 stages in flight), 40 KiB of LDS.  Round 2 measured 17 other ring
+// shapes, a software-pipelined and a de-interleaved variant (profiles/r02d_stream_ring_sweep.txt,
+// r02d_bench_ring_ab.txt); none beat this one and they were removed from the library (round 3).
 // ------------------------------------------------------------------------------------
-template <int OFF>
-__device__ __forceinline__ f32x4 lds_rd(uint32_t a) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
-  f32x4 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF) : "memory");
-  return r;
-}
-
-// Wait until at most N LDS operations are outstanding.  The registers the wait completes are
-// tied through it, so the compiler neither reads them earlier nor reuses them meanwhile (it
-// does not know the reads above were asynchronous).
-template <int N>
-__device__ __forceinline__ void lgk_wait(f32x4& a) {
-  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N));
-}
-template <int N>
-__device__ __forceinline__ void lgk_wait(f32x4& a, f32x4& b) {
-  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
-}
-
-template <class G>
-struct PipeState {
-  float acc[G::D][G::PX];
-  f32x4 A[2];      // f1 quad, double-buffered by channel parity
-  f32x4 Q[5];      // f2 window quads
-  uint32_t aA;     // lane LDS byte addresses (channel 0 of slot 0); slot/channel = immediate
-  uint32_t aW[5];
-};
-
-// The FMAs of one displacement; the scheduling barrier keeps them between the waits and
-// read issues around them (left alone, the scheduler sinks them past the next reads and the
-// stage barrier, lengthening register live ranges until the kernel spills).
-template <class G, int TI>
-__device__ __forceinline__ void pipe_fma(PipeState<G>& s, const f32x4& a) {
-#pragma unroll
-  for (int k = 0; k < G::PX; ++k) {
-    const int j = k + G::S * TI;
-    s.acc[TI][k] = fmaf(a[k], s.Q[j >> 2][j & 3], s.acc[TI][k]);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// Issue reads of the channel stored at immediate offset OFF into A[P] / Q[u].
-template <class G, int OFF, int P>
-__device__ __forceinline__ void pipe_issue_a_q0(PipeState<G>& s) {
-  s.A[P] = lds_rd<OFF>(s.aA);
-  s.Q[0] = lds_rd<OFF>(s.aW[0]);
-}
-
-struct PipeRing {  // per-block constants of the DMA ring
-  const float* img1;
-  const float* img2;
-  uint32_t plane, lds0, img_bytes;
-  int c_begin, wave, nst;
-};
-
-// One channel: slot RS of the unrolled round, channel CI of the stage, runtime stage st.
-template <class G, int RS, int CI>
-__device__ __forceinline__ void pipe_channel(PipeState<G>& s, PipeRing& r, int st,
-                                             const uint32_t (&src_off)[G::PPW],
-                                             const uint32_t (&dst_off)[G::PPW],
-                                             const bool (&from_f2)[G::PPW]) {
-  constexpr int SLOT_B = G::STAGE_FLOATS * 4, CH_B = G::CH_FLOATS * 4;
-  constexpr bool LAST = CI == G::CC - 1;
-  constexpr int NRS = LAST ? (RS + 1) % G::NS : RS;  // next channel's slot and channel
-  constexpr int NCI = LAST ? 0 : CI + 1;
-  constexpr int NOFF = NRS * SLOT_B + NCI * CH_B;
-  constexpr int P = (RS * G::CC + CI) & 1;
-  static_assert((G::NS * G::CC) % 2 == 0, "f1 parity must repeat every round");
-
-  lgk_wait<4>(s.A[P], s.Q[0]);
-  pipe_fma<G, 0>(s, s.A[P]);
-  lgk_wait<3>(s.Q[1]);
-  pipe_fma<G, 1>(s, s.A[P]);
-  if constexpr (LAST) {
-    // stage barrier: stage st+1 must have landed (issuers' counted vmcnt), and every wave is
-    // past all reads of stage st-1, whose slot the DMA for stage st+NS-1 now refills.
-    if (st + 1 < r.nst) {
-      if (r.wave < G::ISSUERS) {
-        if (r.nst - 2 - st >= G::NS - 3)
-          wait_vmcnt<(G::NS - 3) * G::PPW>();
-        else
-          wait_vmcnt<0>();
-      }
-      __builtin_amdgcn_s_barrier();
-      if (st + G::NS - 1 < r.nst)
-        ring_issue<G>(st + G::NS - 1, r.c_begin, r.wave, r.plane, r.lds0, r.img1, r.img2,
-                      r.img_bytes, src_off, dst_off, from_f2);
-    }
-  }
-  // (after the last stage these reads re-read live LDS and are discarded)
-  pipe_issue_a_q0<G, NOFF, P ^ 1>(s);
-  pipe_fma<G, 2>(s, s.A[P]);
-  lgk_wait<4>(s.Q[2]);
-  pipe_fma<G, 3>(s, s.A[P]);
-  s.Q[1] = lds_rd<NOFF>(s.aW[1]);
-  pipe_fma<G, 4>(s, s.A[P]);
-  lgk_wait<4>(s.Q[3]);
-  pipe_fma<G, 5>(s, s.A[P]);
-  s.Q[2] = lds_rd<NOFF>(s.aW[2]);
-  pipe_fma<G, 6>(s, s.A[P]);
-  lgk_wait<4>(s.Q[4]);
-  pipe_fma<G, 7>(s, s.A[P]);
-  s.Q[3] = lds_rd<NOFF>(s.aW[3]);
-  pipe_fma<G, 8>(s, s.A[P]);
-  s.Q[4] = lds_rd<NOFF>(s.aW[4]);
-}
-
-template <class G, int RS, int CI>
-__device__ __forceinline__ void pipe_stage(PipeState<G>& s, PipeRing& r, int st,
-                                           const uint32_t (&src_off)[G::PPW],
-                                           const uint32_t (&dst_off)[G::PPW],
-                                           const bool (&from_f2)[G::PPW]) {
-  if constexpr (CI < G::CC) {
-    pipe_channel<G, RS, CI>(s, r, st, src_off, dst_off, from_f2);
-    pipe_stage<G, RS, CI + 1>(s, r, st, src_off, dst_off, from_f2);
-  }
-}
-
-// Stages st0+RS .. st0+NS-1 of one unrolled round; false once the block's stages are done.
-template <class G, int RS>
-__device__ __forceinline__ bool pipe_round(PipeState<G>& s, PipeRing& r, int st0,
-                                           const uint32_t (&src_off)[G::PPW],
-                                           const uint32_t (&dst_off)[G::PPW],
-                                           const bool (&from_f2)[G::PPW]) {
-  if constexpr (RS < G::NS) {
-    if (st0 + RS >= r.nst) return false;
-    pipe_stage<G, RS, 0>(s, r, st0 + RS, src_off, dst_off, from_f2);
-    return pipe_round<G, RS + 1>(s, r, st0, src_off, dst_off, from_f2);
-  }
-  return true;
-}
-
-template <class G>
-__global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ringp(
-    const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
-    int C, int H, int W, int Ho, int Wo, int off, int layout, float divisor, float inv_divisor,
-    int n_ty, int n_tx, int cps, float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  static_assert(G::NS >= 3, "pipelined ring keeps NS-2 stages in flight");
-  static_assert((G::NS - 1) * G::STAGE_FLOATS * 4 + (G::CC - 1) * G::CH_FLOATS * 4 < 65536,
-                "slot/channel offsets must fit the ds offset field");
-
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int tx_tile = t % n_tx;
-  const int ty_tile = (t / n_tx) % n_ty;
-  const int n = t / (n_tx * n_ty);
-  const int oy0 = ty_tile * G::TY, ox0 = tx_tile * G::TX;
-  const int y1 = oy0 + off, x1 = ox0 + off;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int q = threadIdx.x % G::NQ;
-  const int ty = (threadIdx.x / G::NQ) % G::TY;
-  const int tjx = threadIdx.x / (G::NQ * G::TY);
-
-  PipeRing r;
-  r.plane = (uint32_t)(H * W);
-  const uint32_t img_bytes = (uint32_t)C * r.plane * 4u;
-  r.img1 = in1 + (size_t)n * C * r.plane;
-  r.img2 = in2 + (size_t)n * C * r.plane;
-  r.img_bytes = img_bytes;
-  r.lds0 = lds_addr(lds);
-  r.wave = wave;
-
-  uint32_t src_off[G::PPW];
-  uint32_t dst_off[G::PPW];
-  bool from_f2[G::PPW];
-  constexpr uint32_t kOOB = 0x80000000u;
-  if (wave < G::ISSUERS) {
-#pragma unroll
-    for (int i = 0; i < G::PPW; ++i) {
-      const int p = wave * G::PPW + i;
-      const int cc = p / (G::F2P + G::F1P);
-      const int k = p % (G::F2P + G::F1P);
-      int gy, gx;
-      uint32_t dst = (uint32_t)(cc * G::CH_FLOATS) * 4u;
-      if (k < G::F2P) {
-        const int rr = 8 * k + (lane >> 3);
-        const int srcq = (lane & 7) ^ (((rr >> 1) & 1) << 2);
-        gy = y1 - G::HALO + rr;
-        gx = x1 - G::HALO + 4 * srcq;
-        dst += (uint32_t)(8 * k * G::X2) * 4u;
-      } else {
-        gy = y1 + (lane >> 2);
-        gx = x1 + 4 * (lane & 3);
-        dst += (uint32_t)G::F2_FLOATS * 4u;
-      }
-      const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
-      src_off[i] = ok ? ((uint32_t)cc * r.plane + (uint32_t)(gy * W + gx)) * 4u : kOOB;
-      dst_off[i] = dst;
-      from_f2[i] = k < G::F2P;
-    }
-  }
-
-  PipeState<G> s;
-  const int r2 = ty + G::S * tjx;
-  const int sw = ((r2 >> 1) & 1) << 2;
-#pragma unroll
-  for (int u = 0; u < 5; ++u)
-    s.aW[u] = r.lds0 + (uint32_t)(r2 * G::X2 + (((q + u) ^ sw) << 2)) * 4u;
-  s.aA = r.lds0 + (uint32_t)(G::F2_FLOATS + ty * G::TX + (q << 2)) * 4u;
-#pragma unroll
-  for (int a = 0; a < G::D; ++a)
-#pragma unroll
-    for (int k = 0; k < G::PX; ++k) s.acc[a][k] = 0.f;
-
-  r.c_begin = blockIdx.y * cps;
-  const int c_end = min(C, r.c_begin + cps);
-  r.nst = (c_end - r.c_begin + G::CC - 1) / G::CC;
-  if (r.nst > 0) {
-#pragma unroll
-    for (int st = 0; st < G::NS - 1; ++st)
-      if (st < r.nst)
-        ring_issue<G>(st, r.c_begin, wave, r.plane, r.lds0, r.img1, r.img2, r.img_bytes, src_off,
-                      dst_off, from_f2);
-    if (wave < G::ISSUERS) {
-      if (r.nst - 1 >= G::NS - 2)
-        wait_vmcnt<(G::NS - 2) * G::PPW>();
-      else
-        wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    pipe_issue_a_q0<G, 0, 0>(s);
-#pragma unroll
-    for (int u = 1; u < 5; ++u) s.Q[u] = lds_rd<0>(s.aW[u]);
-    for (int st0 = 0;; st0 += G::NS)
-      if (!pipe_round<G, 0>(s, r, st0, src_off, dst_off, from_f2)) break;
-    // drain the discarded reads before their registers can be reused
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(s.A[0]), "+v"(s.A[1]), "+v"(s.Q[0]), "+v"(s.Q[1]), "+v"(s.Q[2]),
-                   "+v"(s.Q[3]), "+v"(s.Q[4]));
-  }
-
-  const int oy = oy0 + ty;
-  const int ox = ox0 + 4 * q;
-  if (oy >= Ho || ox >= Wo) return;
-  const int OC = G::D * G::D;
-  const int tj = tjx - G::DR;
-  if (gridDim.y > 1) {
-    float* pk = partial + (size_t)blockIdx.y * ((size_t)gridDim.x / (n_tx * n_ty)) * OC * Ho * Wo;
-#pragma unroll
-    for (int ti = 0; ti < G::D; ++ti) {
-      const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
-      *reinterpret_cast<float4*>(pk + (((size_t)n * OC + oc) * Ho + oy) * Wo + ox) =
-          make_float4(s.acc[ti][0], s.acc[ti][1], s.acc[ti][2], s.acc[ti][3]);
-    }
-    return;
-  }
-  const bool pow2 = inv_divisor != 0.f;
-#pragma unroll
-  for (int ti = 0; ti < G::D; ++ti) {
-    const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
-    float4 v;
-    if (pow2)
-      v = make_float4(s.acc[ti][0] * inv_divisor, s.acc[ti][1] * inv_divisor,
-                      s.acc[ti][2] * inv_divisor, s.acc[ti][3] * inv_divisor);
-    else
-      v = make_float4(s.acc[ti][0] / divisor, s.acc[ti][1] / divisor, s.acc[ti][2] / divisor,
-                      s.acc[ti][3] / divisor);
-    *reinterpret_cast<float4*>(out + (((size_t)n * OC + oc) * Ho + oy) * Wo + ox) = v;
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// De-interleaved ring kernel (S == 2): same tile / wave structure, but every lane owns 4
-// SAME-PARITY pixels x = 8q + p + 2k, so its f2 window is 4 + 2*DR = 12 consecutive values of
-// one parity phase: 3 ds_read_b128 + 1 for f1 (4 reads / 36 FMA instead of 6).  The LDS rows
-// are stored phase-split ([quad][phase][4], f2 XOR-swizzled as above), which 16-byte DMA
-// cannot produce, so stages are filled by dword LDS-DMA (buffer_load_dword ... lds) whose
-// per-lane source addresses perform the de-interleave.  Output pairs are swapped between the
-// two phase lanes with one DPP quad_perm so the stores stay float4.
-// ------------------------------------------------------------------------------------
-template <int TY_, int CC_, int NS_, int ISS_>
-struct RingDiTile {
-  static constexpr int DR = 4, S = 2, TY = TY_, CC = CC_, NS = NS_, ISSUERS = ISS_;
-  static constexpr int D = 2 * DR + 1;
-  static constexpr int HALO = DR * S;
-  static constexpr int TX = 16, NG = 4, PX = 4;
-  static constexpr int X2 = 32;
-  static constexpr int R2 = TY + 2 * HALO;
-  static constexpr int NWQ = (PX + 2 * DR) / 4;  // 3 window quads per lane
-  static constexpr int THREADS = TY * NG * D;
-  static constexpr int F2_FLOATS = R2 * X2;
-  static constexpr int F1_FLOATS = TY * TX;
-  static constexpr int CH_FLOATS = F2_FLOATS + F1_FLOATS;
-  static constexpr int STAGE_FLOATS = CC * CH_FLOATS;
-  static constexpr int LDS_BYTES = NS * STAGE_FLOATS * 4;
-  static constexpr int F2P = F2_FLOATS / 64;  // dword pieces (64 floats) per channel
-  static constexpr int F1P = F1_FLOATS / 64;
-  static constexpr int PIECES = CC * (F2P + F1P);
-  static constexpr int PPW = PIECES / ISSUERS;
-  static_assert(PIECES % ISSUERS == 0, "uniform pieces per issuing wave");
-  static_assert(ISSUERS <= THREADS / 64, "enough waves to issue");
-  static_assert((NS - 2) * PPW <= 63, "vmcnt range");
-  static_assert(TX + 2 * HALO == X2 && TY * NG == 64, "one wave per displacement row");
-  static_assert(NS >= 2, "ring depth");
-};
-
-// Six-register variant of the stage read: f1 quad + 3 window quads.
-template <int OFF>
-__device__ __forceinline__ void lds_read4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                          f32x4& r0, f32x4& r1, f32x4& r2, f32x4& r3) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
-  asm volatile(
-      "ds_read_b128 %0, %4 offset:%8\n\t"
-      "ds_read_b128 %1, %5 offset:%8\n\t"
-      "ds_read_b128 %2, %6 offset:%8\n\t"
-      "ds_read_b128 %3, %7 offset:%8\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
-      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "n"(OFF)
-      : "memory");
-}
-
-template <class G, int CC_I>
-__device__ __forceinline__ void ringdi_stage(const uint32_t (&addr)[4],
-                                             float (&acc)[G::D][G::PX]) {
-  if constexpr (CC_I < G::CC) {
-    f32x4 a4, b0, b1, b2;
-    lds_read4<CC_I * G::CH_FLOATS * 4>(addr[0], addr[1], addr[2], addr[3], a4, b0, b1, b2);
-    const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-    const float w[12] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
-                         b2.x, b2.y, b2.z, b2.w};
-#pragma unroll
-    for (int ti = 0; ti < G::D; ++ti)
-#pragma unroll
-      for (int k = 0; k < G::PX; ++k) acc[ti][k] = fmaf(av[k], w[k + ti], acc[ti][k]);
-    ringdi_stage<G, CC_I + 1>(addr, acc);
-  }
-}
-
-template <class G>
-__device__ __forceinline__ void ringdi_issue(int stage, int c_begin, int wave, uint32_t plane,
-                                             uint32_t lds0, __amdgpu_buffer_rsrc_t rs1,
-                                             __amdgpu_buffer_rsrc_t rs2,
-                                             const uint32_t (&src_off)[G::PPW],
-                                             const uint32_t (&dst_off)[G::PPW],
-                                             const bool (&from_f2)[G::PPW]) {
-  constexpr uint32_t kOOB = 0x80000000u;
-  if (wave >= G::ISSUERS) return;
-  const uint32_t cbytes = (uint32_t)(c_begin + stage * G::CC) * plane * 4u;
-  const uint32_t sbase = lds0 + (uint32_t)((stage % G::NS) * G::STAGE_FLOATS) * 4u;
-#pragma unroll
-  for (int i = 0; i < G::PPW; ++i) {
-    const uint32_t vo = src_off[i] == kOOB ? kOOB : src_off[i] + cbytes;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        from_f2[i] ? rs2 : rs1,
-        (__attribute__((address_space(3))) void*)(uintptr_t)(sbase + dst_off[i]), 4, vo, 0, 0,
-        0);
-  }
-}
-
-template <class G>
-__global__ __launch_bounds__(G::THREADS, 6) void corr_fwd_ringdi(
-    const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
-    int C, int H, int W, int Ho, int Wo, int off, int layout, float divisor, float inv_divisor,
-    int n_ty, int n_tx, int cps, float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int tx_tile = t % n_tx;
-  const int ty_tile = (t / n_tx) % n_ty;
-  const int n = t / (n_tx * n_ty);
-  const int oy0 = ty_tile * G::TY, ox0 = tx_tile * G::TX;
-  const int y1 = oy0 + off, x1 = ox0 + off;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = threadIdx.x % G::NG;
-  const int p = g & 1, q = g >> 1;
-  const int ty = (threadIdx.x / G::NG) % G::TY;
-  const int tjx = threadIdx.x / (G::NG * G::TY);
-
-  const uint32_t plane = (uint32_t)(H * W);
-  const uint32_t img_bytes = (uint32_t)C * plane * 4u;
-  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(in1 + (size_t)n * C * plane), (short)0, (int)img_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(in2 + (size_t)n * C * plane), (short)0, (int)img_bytes, 0x00020000);
-  const uint32_t lds0 = lds_addr(lds);
-
-  // dword DMA plan: LDS float F of a channel block <- the image element that belongs there.
-  uint32_t src_off[G::PPW];
-  uint32_t dst_off[G::PPW];
-  bool from_f2[G::PPW];
-  constexpr uint32_t kOOB = 0x80000000u;
-  if (wave < G::ISSUERS) {
-#pragma unroll
-    for (int i = 0; i < G::PPW; ++i) {
-      const int pc = wave * G::PPW + i;
-      const int cc = pc / (G::F2P + G::F1P);
-      const int k = pc % (G::F2P + G::F1P);
-      int gy, gx;
-      uint32_t dst = (uint32_t)(cc * G::CH_FLOATS) * 4u;
-      if (k < G::F2P) {
-        const int F = k * 64 + lane;
-        const int r = F / G::X2, pos = F % G::X2;
-        const int slot = (pos >> 2) ^ (((r >> 1) & 1) << 2);
-        const int m = 4 * (slot >> 1) + (pos & 3);
-        gy = y1 - G::HALO + r;
-        gx = x1 - G::HALO + 2 * m + (slot & 1);
-        dst += (uint32_t)(k * 64) * 4u;
-      } else {
-        const int F = (k - G::F2P) * 64 + lane;
-        const int r = F / G::TX, pos = F % G::TX;
-        const int slot = pos >> 2;
-        const int m = 4 * (slot >> 1) + (pos & 3);
-        gy = y1 + r;
-        gx = x1 + 2 * m + (slot & 1);
-        dst += (uint32_t)(G::F2_FLOATS + (k - G::F2P) * 64) * 4u;
-      }
-      const bool ok = gy >= 0 && gy < H && gx >= 0 && gx < W;
-      src_off[i] = ok ? ((uint32_t)cc * plane + (uint32_t)(gy * W + gx)) * 4u : kOOB;
-      dst_off[i] = dst;
-      from_f2[i] = k < G::F2P;
-    }
-  }
-
-  // LDS read offsets: f1 slot (q, p); window quads q..q+2 of phase p in f2 row ty + 2*tj.
-  const int r2 = ty + G::S * tjx;
-  const int sw = ((r2 >> 1) & 1) << 2;
-  const uint32_t aoff = (uint32_t)(G::F2_FLOATS + ty * G::TX + ((q * 2 + p) << 2)) * 4u;
-  uint32_t woff[G::NWQ];
-#pragma unroll
-  for (int u = 0; u < G::NWQ; ++u)
-    woff[u] = (uint32_t)(r2 * G::X2 + ((((q + u) * 2 + p) ^ sw) << 2)) * 4u;
-
-  float acc[G::D][G::PX];
-#pragma unroll
-  for (int a = 0; a < G::D; ++a)
-#pragma unroll
-    for (int k = 0; k < G::PX; ++k) acc[a][k] = 0.f;
-
-  const int c_begin = blockIdx.y * cps;
-  const int c_end = min(C, c_begin + cps);
-  const int nst = (c_end - c_begin + G::CC - 1) / G::CC;
-#pragma unroll
-  for (int s = 0; s < G::NS - 1; ++s)
-    if (s < nst)
-      ringdi_issue<G>(s, c_begin, wave, plane, lds0, rs1, rs2, src_off, dst_off, from_f2);
-
-  for (int st = 0; st < nst; ++st) {
-    if (wave < G::ISSUERS) {
-      if (nst - 1 - st >= G::NS - 2)
-        wait_vmcnt<(G::NS - 2) * G::PPW>();
-      else
-        wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (st + G::NS - 1 < nst)
-      ringdi_issue<G>(st + G::NS - 1, c_begin, wave, plane, lds0, rs1, rs2, src_off, dst_off,
-                      from_f2);
-    const uint32_t sb = lds0 + (uint32_t)((st % G::NS) * G::STAGE_FLOATS) * 4u;
-    const uint32_t addr[4] = {sb + aoff, sb + woff[0], sb + woff[1], sb + woff[2]};
-    ringdi_stage<G, 0>(addr, acc);
-  }
-
-  // ---- epilogue: lanes p=0 / p=1 of a pair hold the even / odd pixels of 8q..8q+7; one DPP
-  // swap makes lane p=0 own 8q..8q+3 and lane p=1 own 8q+4..8q+7 as float4s ----
-  const int oy = oy0 + ty;
-  const int ox = ox0 + 8 * q + 4 * p;
-  const int OC = G::D * G::D;
-  const int tj = tjx - G::DR;
-  const bool split = gridDim.y > 1;
-  const bool pow2 = inv_divisor != 0.f;
-  float* base = split ? partial + (size_t)blockIdx.y * ((size_t)gridDim.x / (n_tx * n_ty)) *
-                                      OC * Ho * Wo
-                      : out;
-#pragma unroll
-  for (int ti = 0; ti < G::D; ++ti) {
-    // send what the partner needs: p=0 sends its k=2,3 (x 8q+4, 8q+6); p=1 its k=0,1
-    const float s0 = p ? acc[ti][0] : acc[ti][2];
-    const float s1 = p ? acc[ti][1] : acc[ti][3];
-    const float r0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xF, 0xF,
-                                                             false));  // quad_perm [1,0,3,2]
-    const float r1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s1), 0xB1, 0xF, 0xF,
-                                                             false));
-    float4 v = p ? make_float4(r0, acc[ti][2], r1, acc[ti][3])
-                 : make_float4(acc[ti][0], r0, acc[ti][1], r1);
-    if (oy >= Ho || ox >= Wo) continue;
-    if (!split) {
-      if (pow2) {
-        v.x *= inv_divisor; v.y *= inv_divisor; v.z *= inv_divisor; v.w *= inv_divisor;
-      } else {
-        v.x /= divisor; v.y /= divisor; v.z /= divisor; v.w /= divisor;
-      }
-    }
-    const int oc = out_channel(layout, tj, ti - G::DR, G::DR, G::D, G::S);
-    *reinterpret_cast<float4*>(base + (((size_t)n * OC + oc) * Ho + oy) * Wo + ox) = v;
-  }
-}
-
-template <class G>
-static hipError_t launch_ringdi(const void* in1, const void* in2, void* out, int B, int C,
-                                int H, int W, int Ho, int Wo, int off, int layout,
-                                float divisor, int nsplit, void* partial, hipStream_t stream) {
-  const int n_ty = (Ho + G::TY - 1) / G::TY;
-  const int n_tx = (Wo + G::TX - 1) / G::TX;
-  const long long nblk = (long long)B * n_ty * n_tx;
-  if (nblk <= 0) return hipSuccess;
-  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_ringdi<G>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       G::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int nchunks = (C + G::CC - 1) / G::CC;
-  if (nsplit > nchunks) nsplit = nchunks;
-  if (nsplit < 1) nsplit = 1;
-  const int cps = ((nchunks + nsplit - 1) / nsplit) * G::CC;
-  nsplit = (C + cps - 1) / cps;
-  int ex;
-  const float m = std::frexp(divisor, &ex);
-  const float inv = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  take_launch_events(&ev0, &ev1);
-  hipExtLaunchKernelGGL((corr_fwd_ringdi<G>), dim3((unsigned)nblk, (unsigned)nsplit),
-                        dim3(G::THREADS), G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1,
-                        (const float*)in2, (float*)out, C, H, W, Ho, Wo, off, layout, divisor,
-                        inv, n_ty, n_tx, cps, (float*)partial);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || nsplit == 1) return e;
-  return corr_reduce_splits_f32(partial, out, (size_t)B * G::D * G::D * Ho * Wo, nsplit,
-                                divisor, inv, stream);
-}
-
-using RingDiF = RingDiTile<16, 2, 6, 8>;  // 60 KiB, 5 stages in flight, 5 dword pieces/issuer
-using RingDiG = RingDiTile<16, 4, 3, 8>;  // 60 KiB, 2 in flight, 10 pieces/issuer
-using RingDiH = RingDiTile<16, 3, 5, 6>;  // 75 KiB, 4 in flight, 10 pieces/issuer
-using RingDiI = RingDiTile<16, 2, 8, 8>;  // 80 KiB, 7 in flight
-
-// ------------------------------------------------------------------------------------
-// configurations (CC channels per stage, NS ring depth); selectable for measurement with
-// PWC_RING_CFG=<name> (read once).  LDS = NS * CC * 5 KiB.
-// ------------------------------------------------------------------------------------
-using RingA = RingTile<4, 2, 16, 4, 3, 4>;  // 60 KiB, 2 stages in flight
-using RingB = RingTile<4, 2, 16, 4, 4, 4>;  // 80 KiB, 3 in flight
-using RingC = RingTile<4, 2, 16, 2, 6, 2>;  // 60 KiB, 5 in flight
-using RingD = RingTile<4, 2, 16, 3, 5, 3>;  // 75 KiB, 4 in flight
-using RingE = RingTile<4, 2, 16, 2, 8, 2>;  // 80 KiB, 7 in flight
-// three workgroups per tile (3 tj rows each, 24-row f2 tiles): 3x the workgroups of RingC
-using RingN = RingTile<4, 2, 16, 2, 5, 4, 3>;  // 40 KiB, 4 stages in flight
-using RingO = RingTile<4, 2, 16, 3, 3, 4, 3>;  // 36 KiB, 2 in flight
-using RingP = RingTile<4, 2, 16, 2, 4, 4, 3>;  // 32 KiB, 3 in flight
-using RingQ = RingTile<4, 2, 16, 2, 8, 4, 3>;  // 64 KiB: 2 workgroups/CU, later ones staggered
-using RingR = RingTile<4, 2, 16, 2, 14, 4, 3>; // 112 KiB: 1 workgroup/CU
+using RingN = RingTile<4, 2, 16, 2, 5, 4, 3>;
 
 #ifdef PWC_RING_CENSUS
 unsigned* g_census = nullptr;
@@ -974,54 +418,6 @@ static hipError_t launch_ring(const void* in1, const void* in2, void* out, int B
                                 divisor, inv, stream);
 }
 
-template <class G>
-static hipError_t launch_ringp(const void* in1, const void* in2, void* out, int B, int C, int H,
-                               int W, int Ho, int Wo, int off, int layout, float divisor,
-                               int nsplit, void* partial, hipStream_t stream) {
-  const int n_ty = (Ho + G::TY - 1) / G::TY;
-  const int n_tx = (Wo + G::TX - 1) / G::TX;
-  const long long nblk = (long long)B * n_ty * n_tx;
-  if (nblk <= 0) return hipSuccess;
-  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_ringp<G>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       G::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int nchunks = (C + G::CC - 1) / G::CC;
-  if (nsplit > nchunks) nsplit = nchunks;
-  if (nsplit < 1) nsplit = 1;
-  const int cps = ((nchunks + nsplit - 1) / nsplit) * G::CC;
-  nsplit = (C + cps - 1) / cps;
-  int ex;
-  const float m = std::frexp(divisor, &ex);
-  const float inv = (m == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  take_launch_events(&ev0, &ev1);
-  hipExtLaunchKernelGGL((corr_fwd_ringp<G>), dim3((unsigned)nblk, (unsigned)nsplit),
-                        dim3(G::THREADS), G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1,
-                        (const float*)in2, (float*)out, C, H, W, Ho, Wo, off, layout, divisor,
-                        inv, n_ty, n_tx, cps, (float*)partial);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || nsplit == 1) return e;
-  return corr_reduce_splits_f32(partial, out, (size_t)B * G::D * G::D * Ho * Wo, nsplit,
-                                divisor, inv, stream);
-}
-
-using RingPJ = RingTile<4, 2, 16, 2, 6, 2>;   // 60 KiB, 4 stages (8 channels) in flight
-using RingPK = RingTile<4, 2, 16, 1, 12, 1>;  // 60 KiB, 10 single-channel stages in flight
-using RingPL = RingTile<4, 2, 16, 3, 4, 3>;   // 60 KiB, 2 stages (6 channels) in flight
-using RingPM = RingTile<4, 2, 16, 2, 5, 2>;   // 50 KiB, 3 stages (6 channels) in flight
-
-static int ring_cfg() {
-  // knob ring_cfg = 0..17 (A..R); default 13 = N (3 workgroups per tile; measured 18.3 vs
-  // 19.9 us for C at l4, B 8)
-  return debug_knob("ring_cfg", 13);
-}
-
 // Number of channel splits for a grid of `base_blocks` tiles: none once the tiles alone give
 // every CU a workgroup; otherwise aim at two workgroups per CU (512), at most one split per
 // channel chunk and at most `max_splits` (the caller sizes max_splits so that the partial
@@ -1047,28 +443,8 @@ hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, in
   if ((size_t)C * H * W * 4 >= 0x7ffffff0ull) return hipErrorNotSupported;
   const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
   const int ns = partial ? corr_pick_splits(tiles, (C + 3) / 4, max_splits) : 1;
-  const int rc = ring_cfg();
-  if (!epi_is_default(current_epi()) && rc >= 5 && rc <= 12) return hipErrorNotSupported;
-  switch (rc) {
-    case 0: return launch_ring<RingA>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 1: return launch_ring<RingB>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 3: return launch_ring<RingD>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 4: return launch_ring<RingE>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 5: return launch_ringdi<RingDiF>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 6: return launch_ringdi<RingDiG>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 7: return launch_ringdi<RingDiH>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 8: return launch_ringdi<RingDiI>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 9: return launch_ringp<RingPJ>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 10: return launch_ringp<RingPK>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 11: return launch_ringp<RingPL>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 12: return launch_ringp<RingPM>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 14: return launch_ring<RingO>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 15: return launch_ring<RingP>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 16: return launch_ring<RingQ>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 17: return launch_ring<RingR>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    case 2: return launch_ring<RingC>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-    default: return launch_ring<RingN>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial, stream);
-  }
+  return launch_ring<RingN>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, ns, partial,
+                           stream);
 }
 
 }  // namespace pwc

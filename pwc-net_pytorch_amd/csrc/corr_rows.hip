@@ -308,9 +308,9 @@ __global__ __launch_bounds__(NT, 1) void corr_fwd_rows_pair(RowsArgs a, RowsArgs
 
 }  // namespace rows
 
-// Serves l3-sized grids (13..24 parity rows per image) by default.  PWC_ROWS=0 disables the
-// kernel, PWC_ROWS=1 selects it at every size >= 13 parity rows, PWC_ROWS_CFG="R,CK" forces
-// a configuration at any size (measurement).
+// Serves l2/l3-sized grids (7..24 parity rows per image) by default.  Measurement knobs: rows=0
+// disables the kernel, rows=2 selects it at every size; rows_r / rows_ck / rows_ts force a
+// configuration.
 // dtype 0: fp32 storage, 1: fp16 (Sintel l0..l2 of config 4: every parity-row count, W % 8).
 namespace rows {
 struct Plan {
@@ -405,6 +405,33 @@ static hipError_t plan(int B, int C, int H, int W, float divisor, int dtype, Pla
 }
 }  // namespace rows
 
+// The instantiated (storage type, band rows R, loads per thread M1 / M2) variants, first match
+// wins: the launcher and the acceptance predicate below walk the same list.
+#define PWC_ROWS_VARIANTS(X)                                                  \
+  X(float, 3, 2, 7) /* l4 at CK 16: 1.75 / 6.4 loads per thread per chunk */ \
+  X(float, 3, 1, 4) /* CK 8 */                                               \
+  X(float, 2, 2, 6)                                                          \
+  X(float, 2, 1, 3)                                                          \
+  X(float, 1, 1, 5)                                                          \
+  X(float, 4, 2, 8)                                                          \
+  X(float, 2, 2, 8)                                                          \
+  X(float, 1, 2, 8)                                                          \
+  X(_Float16, 2, 1, 3)                                                       \
+  X(_Float16, 2, 2, 6)                                                       \
+  X(_Float16, 1, 1, 3)                                                       \
+  X(_Float16, 1, 2, 5)
+
+// Whether corr_forward_rows serves this problem (a plan and an instantiated variant exist).
+bool corr_rows_accepts(int B, int C, int H, int W, int dtype) {
+  rows::Plan P;
+  if (rows::plan(B, C, H, W, (float)C, dtype, &P) != hipSuccess) return false;
+#define PWC_ROWS_OK(TT, RR, M1, M2) \
+  if (sizeof(TT) == (P.h16 ? 2u : 4u) && P.R == RR && P.per1 <= M1 && P.per2 <= M2) return true;
+  PWC_ROWS_VARIANTS(PWC_ROWS_OK)
+#undef PWC_ROWS_OK
+  return false;
+}
+
 hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B, int C, int H,
                              int W, float divisor, int dtype, hipStream_t stream) {
   using namespace rows;
@@ -434,18 +461,7 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
                           (TT*)out, C, H, W, divisor, inv, g, current_epi());                 \
     return hipGetLastError();                                                                 \
   }
-  PWC_ROWS(float, 3, 2, 7)   // l4 at CK 16: 1.75 / 6.4 loads per thread per chunk
-  PWC_ROWS(float, 3, 1, 4)   // CK 8
-  PWC_ROWS(float, 2, 2, 6)
-  PWC_ROWS(float, 2, 1, 3)
-  PWC_ROWS(float, 1, 1, 5)
-  PWC_ROWS(float, 4, 2, 8)
-  PWC_ROWS(float, 2, 2, 8)
-  PWC_ROWS(float, 1, 2, 8)
-  PWC_ROWS(_Float16, 2, 1, 3)
-  PWC_ROWS(_Float16, 2, 2, 6)
-  PWC_ROWS(_Float16, 1, 1, 3)
-  PWC_ROWS(_Float16, 1, 2, 5)
+  PWC_ROWS_VARIANTS(PWC_ROWS)
 #undef PWC_ROWS
   return hipErrorNotSupported;
 }

@@ -769,13 +769,10 @@ static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C
   // stride-1 displacements (Corr4, CostVolumeLayer): the 4 x 4 ring needs more than the 256
   // VGPRs (~640 spilled to scratch), 2 x 4 none, at the same time (l4 16.9-17.0 us against
   // 16.9-17.3 over 300 launches each; profiles/r02e_corr4_ring.txt)
-  const int dcfg = S2 == 1 ? 2 : 0;
-  switch (debug_knob("stream_cfg", dcfg)) {  // measurement variants (CC, NS)
-    case 2: return launch<Geo<T, S2, 3, TWP, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    case 8: return launch<Geo<T, S2, 3, TWP, 2, 8>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    case 4: return launch<Geo<T, S2, 3, TWP, 4, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-    default: return launch<Geo<T, S2, 3, TWP, 4, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-  }
+  if constexpr (S2 == 1)
+    return launch<Geo<T, S2, 3, TWP, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+  else
+    return launch<Geo<T, S2, 3, TWP, 4, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
 }
 
 }  // namespace stream
@@ -786,18 +783,25 @@ static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C
 // CVL channel order); fp32 or fp16 storage (dtype 0 / 1); W a multiple of 4 (fp32) or 8
 // (fp16) and 16-B aligned pointers; C a multiple of 16; grids of at least ~one workgroup per
 // CU (smaller grids have faster homes: corr_pt / corr_rows).
-hipError_t corr_forward_stream(const void* in1, const void* in2, void* out, int B, int C, int H,
-                               int W, int s2, int dtype, int layout, float divisor,
-                               hipStream_t stream) {
+// Whether corr_forward_stream serves this problem (also the pairing predicate of the group
+// entry, capi.hip, through corr_forward_path).
+bool corr_stream_accepts(const void* in1, const void* in2, const void* out, int B, int C, int H,
+                         int W, int s2, int dtype) {
   const int epq = dtype == 1 ? 8 : 4;
-  if (dtype != 0 && dtype != 1) return hipErrorNotSupported;
-  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16 || W % epq)
-    return hipErrorNotSupported;
-  if ((size_t)C * H * W * (16 / epq) >= 0x7ffffff0ull || C % 16) return hipErrorNotSupported;
+  if (dtype != 0 && dtype != 1) return false;
+  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16 || W % epq) return false;
+  if ((size_t)C * H * W * (16 / epq) >= 0x7ffffff0ull || C % 16) return false;
   const int twp = (W % 112 == 0 || W < 112) ? 112 : 128;  // column tile width in pixels
   const long long nblk = (long long)B * (s2 == 2 ? 2 : 1) *
                          (((s2 == 2 ? (H + 1) / 2 : H) + 2) / 3) * ((W + twp - 1) / twp);
-  if (nblk < 192 || W < 64) return hipErrorNotSupported;
+  return nblk >= 192 && W >= 64 && (s2 == 1 || s2 == 2);
+}
+
+hipError_t corr_forward_stream(const void* in1, const void* in2, void* out, int B, int C, int H,
+                               int W, int s2, int dtype, int layout, float divisor,
+                               hipStream_t stream) {
+  if (!corr_stream_accepts(in1, in2, out, B, C, H, W, s2, dtype)) return hipErrorNotSupported;
+  const int twp = (W % 112 == 0 || W < 112) ? 112 : 128;  // column tile width in pixels
   using namespace stream;
 #define PWC_PICK(T)                                                                            \
   if (s2 == 2)                                                                                 \

@@ -26,6 +26,11 @@ template <> __device__ __forceinline__ __hip_bfloat16 from_f32<__hip_bfloat16>(f
 //   CVL:    modules.py:58-72 CostVolumeLayer order, displacement (dy,dx) = (tj*s2, ti*s2)
 enum Layout : int { kRaster = 0, kCvl = 1 };
 
+// The correlation forward's first dispatch stages (corr_fwd.hip, corr_forward_path).
+enum CorrPath : int { kPathOther = 0, kPathStream = 1, kPathBand = 2, kPathRows = 3 };
+int corr_forward_path(const void* in1, const void* in2, const void* out, int B, int C, int H,
+                      int W, int pad, int k, int md, int s1, int s2, int layout, int dtype);
+
 // CostVolumeLayer channel of displacement (dy, dx) for search range sr (modules.py:58-72):
 // 0 -> (0,0); for i = 1..sr the block of 4+4*sr channels starting at 1+(i-1)*(4+4sr) holds
 // (-i,0),(+i,0),(0,-i),(0,+i) then for j = 1..sr (-i,-j),(+i,+j),(-i,+j),(+i,-j).

@@ -224,62 +224,6 @@ __global__ __launch_bounds__(256) void warp_fwd_group(WarpGroupArgs<T> a) {
                                    cy);
 }
 
-// fp32 only: grad_x accumulated with atomics (zeroed by the launcher), grad_flow per pixel.
-// Channels are processed CB at a time with all loads of a group issued together.
-template <int CB>
-__global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
-                                                       const float* __restrict__ flow,
-                                                       const float* __restrict__ gout,
-                                                       float* __restrict__ gx,
-                                                       float* __restrict__ gflow, int B, int C,
-                                                       int H, int W, float halfx, float halfy) {
-  const unsigned plane = (unsigned)(H * W);
-  const unsigned idx = blockIdx.x * 256u + threadIdx.x;
-  if (idx >= (unsigned)B * plane) return;
-  const unsigned n = idx / plane;
-  const unsigned pix = idx - n * plane;
-  const int py = (int)(pix / (unsigned)W);
-  const int px = (int)pix - py * W;
-  const float u = flow[(2 * n + 0) * plane + pix];
-  const float v = flow[(2 * n + 1) * plane + pix];
-  const float ix = src_coord(u, px, W, halfx);
-  const float iy = src_coord(v, py, H, halfy);
-  const Bilinear b = bilinear(ix, iy, H, W);
-  const Corners k = corners(b, H, W);
-  const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;
-  const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
-  float gix = 0.f, giy = 0.f;
-  for (int c0 = 0; c0 < C; c0 += CB) {
-    float r[CB][4], go[CB];
-#pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int c = min(c0 + i, C - 1);
-      const float* p = x + ((unsigned)(n * C + c)) * plane;
-      r[i][0] = masked(p[k.i00], k.m00);
-      r[i][1] = masked(p[k.i01], k.m01);
-      r[i][2] = masked(p[k.i10], k.m10);
-      r[i][3] = masked(p[k.i11], k.m11);
-      go[i] = (c0 + i < C) ? gout[((unsigned)(n * C + c)) * plane + pix] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      if (c0 + i >= C) break;
-      float* q = gx + ((unsigned)(n * C + c0 + i)) * plane;
-      if (k.m00 != 0.f) atomicAdd(q + k.i00, go[i] * w00);
-      if (k.m01 != 0.f) atomicAdd(q + k.i01, go[i] * w01);
-      if (k.m10 != 0.f) atomicAdd(q + k.i10, go[i] * w10);
-      if (k.m11 != 0.f) atomicAdd(q + k.i11, go[i] * w11);
-      gix += go[i] * ((r[i][1] - r[i][0]) * b.wy0 + (r[i][3] - r[i][2]) * b.wy1);
-      giy += go[i] * ((r[i][2] - r[i][0]) * b.wx0 + (r[i][3] - r[i][1]) * b.wx1);
-    }
-  }
-  // grid grad (ATen: * (size-1)/2) then through flow / ((size-1)/2): net factor 1 in exact
-  // arithmetic; keep the two fp32 roundings of the reference chain.
-  const float mx = (float)(W - 1) / 2.f, my = (float)(H - 1) / 2.f;
-  gflow[(2 * n + 0) * plane + pix] = (gix * mx) / halfx;
-  gflow[(2 * n + 1) * plane + pix] = (giy * my) / halfy;
-}
-
 // ---- backward without a scatter over HBM (fp32) ----
 // grad_x as a gather: a workgroup owns a TH x TW tile of grad_x (one pixel per thread) for
 // CC channels.  Every output pixel within M of the tile (its candidate window) recomputes its
@@ -646,10 +590,6 @@ __global__ __launch_bounds__(256) void warp_bwd_far(const float* __restrict__ fl
   }
 }
 
-// knob warp_cfg selects a (channels per group, groups per thread) variant for measurement:
-// 0 = 4 channels per thread, XCD-grouped pixel blocks (default), 1 = 8, 2 = 2,
-// 3 = 4 without XCD grouping, 4 = 2 grouped, 5 = 8 grouped.
-static int warp_cfg() { return debug_knob("warp_cfg", 0); }
 
 template <typename T>
 hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int C, int H,
@@ -663,28 +603,17 @@ hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int
   hipLaunchKernelGGL((warp_fwd_kernel<T, CB, NG, XCD>),                                       \
                      dim3(gx, (unsigned)((C + CB * NG - 1) / (CB * NG))), dim3(256), 0, stream, \
                      (const T*)x, (const T*)flow, (T*)out, B, C, H, W, halfx, halfy)
-  // fp16 storage on large grids: a thread walks 4 groups of channels (its gathers of the next
-  // group in flight while one is blended) -- config-4 Sintel l4 34.0 -> 27.6 us, l3 18.9 ->
-  // 15.7, l2 9.2 -> 8.6 (B=16) with groups of 4; groups of 2 (more threads) another 3-7 %:
-  // l4 30.3 -> 28.0, l3 16.6 -> 16.2, l2 8.67 -> 8.42 (profiles/r02e_warp_fp16_cfg.txt); fp32
-  // measured best at one group of 4 (r02d_warp_cb_sweep)
-  int cfg = warp_cfg();
-  if (cfg == 0 && sizeof(T) == 2 && npix >= 16384) cfg = 9;
-  // fp32 on large grids: 8 channels per thread (config-2 l3 5.57 -> 5.32 us, l4 equal; l2
-  // stays at 4: 3.52 against 3.68 -- 300 launches each, profiles/r02e_warp_fp32_cfg.txt)
-  if (cfg == 0 && sizeof(T) == 4 && npix >= 16384) cfg = 5;
-  switch (cfg) {
-    case 1: PWC_WARP_LAUNCH(8, 1, false); break;
-    case 2: PWC_WARP_LAUNCH(2, 1, false); break;
-    case 3: PWC_WARP_LAUNCH(4, 1, false); break;
-    case 4: PWC_WARP_LAUNCH(2, 1, true); break;
-    case 5: PWC_WARP_LAUNCH(8, 1, true); break;
-    case 6: PWC_WARP_LAUNCH(4, 2, true); break;
-    case 7: PWC_WARP_LAUNCH(4, 4, true); break;
-    case 8: PWC_WARP_LAUNCH(4, 8, true); break;
-    case 9: PWC_WARP_LAUNCH(2, 4, true); break;
-    default: PWC_WARP_LAUNCH(4, 1, true); break;
-  }
+  // fp16 storage on large grids: a thread walks 4 groups of 2 channels (its gathers of the next
+  // group in flight while one is blended) -- config-4 Sintel l4 34.0 -> 28.0 us, l3 18.9 ->
+  // 16.2, l2 9.2 -> 8.4 (profiles/r02e_warp_fp16_cfg.txt); fp32 on large grids: 8 channels per
+  // thread (config-2 l3 5.57 -> 5.32 us, l4 equal; l2 stays at 4: 3.52 against 3.68 --
+  // profiles/r02e_warp_fp32_cfg.txt).  Other shapes measured in round 2 were removed.
+  if (npix >= 16384 && sizeof(T) == 2)
+    PWC_WARP_LAUNCH(2, 4, true);
+  else if (npix >= 16384)
+    PWC_WARP_LAUNCH(8, 1, true);
+  else
+    PWC_WARP_LAUNCH(4, 1, true);
 #undef PWC_WARP_LAUNCH
   return hipGetLastError();
 }
@@ -705,8 +634,7 @@ hipError_t warp_forward_group_t(const WarpProblem* probs, int count, hipStream_t
       if (npix > big) big = npix;
     }
     // fp32 large grids: 8 channels per thread; fp16 large grids: 4 groups of 2; else 4 x 1
-    // knob warp_group_cpt=4 keeps 4 channels per thread on large grids (measurement)
-    cb8 = big >= 16384 && debug_knob("warp_group_cpt", 8) == 8;
+    cb8 = big >= 16384;
     const int cpt = cb8 ? 8 : 4;
     for (int i = i0; i < count && i < i0 + kWarpGroupMax; ++i) {
       const WarpProblem& q = probs[i];
@@ -752,147 +680,106 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
   if (npix == 0) return hipSuccess;
   if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
   const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
-  const bool scatter = debug_knob("warp_bwd", 1) == 0;  // 0: ATen-shaped atomic scatter
-  if (!scatter) {
-    // grad_x tile shape (knob warp_tiles for measurement)
-    // wide rows (l4: 96 x 112 at 384 x 448) take 16-channel tile groups and two channel groups
-    // in warp_bwd_flow: 55.3 -> 42.8 us at l4; narrower levels measured best at the defaults
-    // (profiles/r02d_bwd_knobs.txt)
-    // (with the per-wave list build, 16 x 16 tiles beat 8 x 32 at l4: 36.5 -> 34.5 us; l3 stays
-    // at 8 x 32, 23.3 against 26.0 -- profiles/r02e_warp_bwd_modes.txt)
-    const bool wide = W >= 96;
+  // Round 2's measured choices (profiles/r02d_bwd_knobs.txt, r02e_warp_bwd_modes.txt,
+  // r02e_warp_bwd_small.txt); the other tile shapes, list-build modes, dword-corner flow loads
+  // and the ATen-shaped atomic scatter were removed from the library in round 3.
+  // wide rows (l4: 96 x 112 at 384 x 448) take 16 x 16 tiles of 16 channels and two channel
+  // groups in warp_bwd_flow; narrower images 8 x 32 tiles of 8 channels
+  const bool wide = W >= 96;
+  // channel groups for grids with few pixels (the coarse levels): ~64K threads or 16 groups
+  int ng = 1;
+  while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
+  if (C > 0) {
     // images inside one grad_x tile (l0 6 x 7 in 8 x 32, l1 12 x 14 in 16 x 16): grad_x and
-    // grad_flow in one merged launch (warp_bwd_small; knob warp_bwd_small=0 for two launches)
-    if (C > 0 && debug_knob("warp_bwd_small", 1) && debug_knob("warp_tiles", -1) < 0 &&
-        debug_knob("wbg_mode", 6) == 6) {
-      int ng = 1;
-      while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
-      const int tws = (H <= 8 && W <= 32) ? 32 : (H <= 16 && W <= 16) ? 16 : 0;
-      if (tws && ng == 16) {
-        const int cc = tws == 32 ? 8 : 16, ncg = (C + cc - 1) / cc, ngx = B * ncg;
-        const int cpg = (C + ng - 1) / ng;
-        const unsigned nflow = (unsigned)((npix * ng + 255) / 256);
-        const dim3 grid((unsigned)ngx + nflow);
-        if (tws == 32)
-          hipLaunchKernelGGL((warp_bwd_small<32, 8, 6, 8, 16, true>), grid, dim3(256), 0, stream,
-                             (const float*)x, (const float*)flow, (const float*)gout, (float*)gx,
-                             (float*)gflow, B, C, H, W, halfx, halfy, cpg, ngx, ncg);
-        else
-          hipLaunchKernelGGL((warp_bwd_small<16, 16, 6, 8, 16, true>), grid, dim3(256), 0,
-                             stream, (const float*)x, (const float*)flow, (const float*)gout,
-                             (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy, cpg, ngx, ncg);
-        return hipGetLastError();
-      }
-    }
-    const int tv = debug_knob("warp_tiles", wide ? 6 : 0);
-    // grad_x tiles and grad_flow in one launch + the far-corner pass (knob warp_bwd_merge)
-    // merged tiles: 16 x 16 from 48-px rows (l3: 720 workgroups, 23.3 -> 21.7 us against the
-    // two launches of 8 x 32 tiles), else 8 x 32 (l2)
-    const int tvm = debug_knob("warp_tiles", W >= 48 ? 6 : 0);
-    if (C > 0 && debug_knob("warp_bwd_merge", 1) && debug_knob("wbg_mode", 6) == 6 &&
-        debug_knob("wbf_pairs", 1) && (tvm == 0 || tvm == 6)) {
-      const int tv = tvm;
-      int ng = 1;
-      while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
-      if (wide && ng == 1 && C >= 32) ng = 2;
-      if (const int k = debug_knob("warp_bwd_ng", 0)) ng = k;
-      const int TWm = tv == 6 ? 16 : 32, CCm = tv == 6 ? 16 : 8, THm = 256 / TWm;
-      const int ntx = (W + TWm - 1) / TWm, nty = (H + THm - 1) / THm, ntiles = ntx * nty;
-      const int ngx = ntiles * B * ((C + CCm - 1) / CCm);
+    // grad_flow in one merged launch (warp_bwd_small; knob warp_bwd_small=0: the general path)
+    const int tws = (H <= 8 && W <= 32) ? 32 : (H <= 16 && W <= 16) ? 16 : 0;
+    if (tws && ng == 16 && debug_knob("warp_bwd_small", 1)) {
+      const int cc = tws == 32 ? 8 : 16, ncg = (C + cc - 1) / cc, ngx = B * ncg;
       const int cpg = (C + ng - 1) / ng;
       const unsigned nflow = (unsigned)((npix * ng + 255) / 256);
-      // only where both halves fit about one round of the chip together: l2 (456 workgroups)
-      // 17.5 -> 13.1 us, l3 (720) 23.3 -> 21.7; l3 with 8 x 32 tiles (1104) 22.8 -> 29.7 and
-      // l4 (1344) 34.8 -> 39.1 measured slower (profiles/r02e_warp_bwd_small.txt)
-      const long long mcap = debug_knob("warp_bwd_mcap", 800);
-      bool done = (long long)ngx + nflow > mcap;
-#define PWC_MERGED(TVV, TW_, CC_, NG_)                                                         \
-  if (!done && tv == TVV && ng == NG_) {                                                       \
-    hipLaunchKernelGGL((warp_bwd_merged<TW_, CC_, 6, 8, NG_, true>), dim3((unsigned)ngx + nflow), \
-                       dim3(256), 0, stream, (const float*)x, (const float*)flow,              \
-                       (const float*)gout, (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy, \
-                       cpg, ntx, ntiles, ngx);                                                 \
-    done = true;                                                                               \
+      const dim3 grid((unsigned)ngx + nflow);
+      if (tws == 32)
+        hipLaunchKernelGGL((warp_bwd_small<32, 8, 6, 8, 16, true>), grid, dim3(256), 0, stream,
+                           (const float*)x, (const float*)flow, (const float*)gout, (float*)gx,
+                           (float*)gflow, B, C, H, W, halfx, halfy, cpg, ngx, ncg);
+      else
+        hipLaunchKernelGGL((warp_bwd_small<16, 16, 6, 8, 16, true>), grid, dim3(256), 0, stream,
+                           (const float*)x, (const float*)flow, (const float*)gout, (float*)gx,
+                           (float*)gflow, B, C, H, W, halfx, halfy, cpg, ngx, ncg);
+      return hipGetLastError();
+    }
   }
-      PWC_MERGED(0, 32, 8, 8)
-      PWC_MERGED(0, 32, 8, 4)
-      PWC_MERGED(0, 32, 8, 2)
-      PWC_MERGED(6, 16, 16, 4)
-      PWC_MERGED(6, 16, 16, 2)
-      PWC_MERGED(6, 16, 16, 1)
+  if (wide && ng == 1 && C >= 32) ng = 2;
+  const int cpg = (C + ng - 1) / ng;
+  const unsigned nflow = (unsigned)((npix * ng + 255) / 256);
+  if (C > 0 && debug_knob("warp_bwd_merge", 1)) {
+    // grad_x tiles and grad_flow in one launch + the far-corner pass, where both halves fit
+    // about one round of the chip together: l2 (456 workgroups) 17.5 -> 13.1 us, l3 (720, 16 x
+    // 16 tiles from 48-px rows) 23.3 -> 21.7; l4 (1344) measured slower
+    const bool t16 = W >= 48;
+    const int TWm = t16 ? 16 : 32, CCm = t16 ? 16 : 8, THm = 256 / TWm;
+    const int ntx = (W + TWm - 1) / TWm, nty = (H + THm - 1) / THm, ntiles = ntx * nty;
+    const int ngx = ntiles * B * ((C + CCm - 1) / CCm);
+    if ((long long)ngx + nflow <= 800) {
+      bool done = false;
+#define PWC_MERGED(T16, TW_, CC_, NG_)                                                          \
+  if (!done && t16 == T16 && ng == NG_) {                                                       \
+    hipLaunchKernelGGL((warp_bwd_merged<TW_, CC_, 6, 8, NG_, true>), dim3((unsigned)ngx + nflow), \
+                       dim3(256), 0, stream, (const float*)x, (const float*)flow,               \
+                       (const float*)gout, (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy,  \
+                       cpg, ntx, ntiles, ngx);                                                  \
+    done = true;                                                                                \
+  }
+      PWC_MERGED(false, 32, 8, 8)
+      PWC_MERGED(false, 32, 8, 4)
+      PWC_MERGED(false, 32, 8, 2)
+      PWC_MERGED(true, 16, 16, 4)
+      PWC_MERGED(true, 16, 16, 2)
+      PWC_MERGED(true, 16, 16, 1)
 #undef PWC_MERGED
-      if (done && (long long)ngx + nflow <= mcap) {
+      if (done) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(warp_bwd_far, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream,
-                           (const float*)flow, (const float*)gout, (float*)gx, B, C, H, W, halfx,
-                           halfy, THm, TWm);
+        hipLaunchKernelGGL(warp_bwd_far, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0,
+                           stream, (const float*)flow, (const float*)gout, (float*)gx, B, C, H,
+                           W, halfx, halfy, THm, TWm);
         return hipGetLastError();
       }
     }
-    int th = 8, tw = 32;
-    if (C > 0) {
-      hipError_t e = hipSuccess;
-      // list build: 6 = per-wave slot counters + buffer-load gathers two entries deep (l4 42.8
-      // -> 36.0 us with the flow kernel's paired loads, l3 28.2 -> 22.8, l2 21.2 -> 17.4:
-      // profiles/r02e_warp_bwd_modes.txt); 0 = the atomic counting sort + insertion sort
-      const int gm = debug_knob("wbg_mode", 6);
-#define PWC_TILES_M(V, TW, CC, M)                                                              \
-  if (tv == V && gm == M) {                                                                    \
-    th = 256 / TW;                                                                             \
-    tw = TW;                                                                                   \
-    const int ntx = (W + TW - 1) / TW, nty = (H + th - 1) / th;                                \
-    hipLaunchKernelGGL((warp_bwd_gx_lists<TW, CC, M>),                                         \
-                       dim3((unsigned)(ntx * nty), (unsigned)B, (unsigned)((C + CC - 1) / CC)), \
-                       dim3(256), 0, stream, (const float*)flow, (const float*)gout,           \
-                       (float*)gx, C, H, W, halfx, halfy, ntx);                                \
-    e = hipGetLastError();                                                                     \
   }
-#define PWC_TILES(V, TW, CC) PWC_TILES_M(V, TW, CC, 0) PWC_TILES_M(V, TW, CC, 6)
-      PWC_TILES(0, 32, 8)
-      PWC_TILES(1, 32, 4)
-      PWC_TILES(2, 32, 16)
-      PWC_TILES(3, 16, 8)
-      PWC_TILES(4, 64, 8)
-      PWC_TILES(5, 32, 32)
-      PWC_TILES(6, 16, 16)
-      PWC_TILES(7, 64, 16)
-#undef PWC_TILES
-#undef PWC_TILES_M
-      if (e != hipSuccess) return e;
-    }
-    // channel groups for grids with few pixels (the coarse levels): ~64K threads or 16 groups
-    int ng = 1;
-    while (ng < 16 && npix * ng < 65536 && C >= 8 * ng * 2) ng *= 2;
-    if (wide && ng == 1 && C >= 32) ng = 2;
-    if (const int k = debug_knob("warp_bwd_ng", 0)) ng = k;
-    const int cpg = (C + ng - 1) / ng;
-    const unsigned blocks = (unsigned)((npix * ng + 255) / 256);
-    const bool fpairs = debug_knob("wbf_pairs", 1) != 0;  // 8-byte corner-pair gathers
-#define PWC_FLOW_P(NGV, PR)                                                                    \
-  if (ng == NGV && fpairs == PR) {                                                             \
-    hipLaunchKernelGGL((warp_bwd_flow<8, NGV, PR>), dim3(blocks), dim3(256), 0, stream,        \
+  // two launches: grad_x tiles (list build with per-wave slot counters, buffer-load gathers two
+  // entries deep), then grad_flow with the far corners
+  const int TW = wide ? 16 : 32, th = 256 / TW;
+  if (C > 0) {
+    const int ntx = (W + TW - 1) / TW, nty = (H + th - 1) / th;
+    if (wide)
+      hipLaunchKernelGGL((warp_bwd_gx_lists<16, 16, 6>),
+                         dim3((unsigned)(ntx * nty), (unsigned)B, (unsigned)((C + 15) / 16)),
+                         dim3(256), 0, stream, (const float*)flow, (const float*)gout, (float*)gx,
+                         C, H, W, halfx, halfy, ntx);
+    else
+      hipLaunchKernelGGL((warp_bwd_gx_lists<32, 8, 6>),
+                         dim3((unsigned)(ntx * nty), (unsigned)B, (unsigned)((C + 7) / 8)),
+                         dim3(256), 0, stream, (const float*)flow, (const float*)gout, (float*)gx,
+                         C, H, W, halfx, halfy, ntx);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const unsigned blocks = nflow;
+#define PWC_FLOW(NGV)                                                                          \
+  if (ng == NGV) {                                                                             \
+    hipLaunchKernelGGL((warp_bwd_flow<8, NGV, true>), dim3(blocks), dim3(256), 0, stream,      \
                        (const float*)x, (const float*)flow, (const float*)gout, (float*)gx,    \
-                       (float*)gflow, B, C, H, W, halfx, halfy, cpg, th, tw);                  \
+                       (float*)gflow, B, C, H, W, halfx, halfy, cpg, th, TW);                  \
     return hipGetLastError();                                                                  \
   }
-#define PWC_FLOW(NGV) PWC_FLOW_P(NGV, false) PWC_FLOW_P(NGV, true)
-    PWC_FLOW(1)
-    PWC_FLOW(2)
-    PWC_FLOW(4)
-    PWC_FLOW(8)
-    PWC_FLOW(16)
+  PWC_FLOW(1)
+  PWC_FLOW(2)
+  PWC_FLOW(4)
+  PWC_FLOW(8)
+  PWC_FLOW(16)
 #undef PWC_FLOW
-#undef PWC_FLOW_P
-    return hipErrorNotSupported;
-  }
-  // PWC_WARP_BWD=0: the scatter of ATen's kernel (global atomics into a zeroed grad_x)
-  hipError_t e = hipMemsetAsync(gx, 0, sizeof(float) * npix * C, stream);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(warp_bwd_kernel<8>, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0,
-                     stream, (const float*)x, (const float*)flow, (const float*)gout,
-                     (float*)gx, (float*)gflow, B, C, H, W, halfx, halfy);
-  return hipGetLastError();
+  return hipErrorNotSupported;
 }
 
 // model.py:78 + :80 in one launch: x2_warp = warp(x2, up2(flow_coarse) * 2), flow_up written

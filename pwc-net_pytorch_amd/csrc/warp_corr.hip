@@ -515,6 +515,16 @@ static bool make_prob(const void* f1, const void* x2, const void* flow, void* x2
 
 }  // namespace band
 
+// Whether the band kernel serves this problem (its geometry fits a workgroup).
+bool warp_corr_band_accepts(int B, int C, int H, int W, int warp) {
+  if (B == 0 || C == 0 || H == 0 || W == 0) return true;
+  band::Prob P;
+  size_t lds;
+  int R = 0, T = 1;
+  return band::make_prob(nullptr, nullptr, nullptr, nullptr, nullptr, B, C, H, W, (float)C, warp,
+                         &R, &T, &P, &lds);
+}
+
 // Fused warp -> correlation for Correlation(pad == md in {8, 9}, k 1, s1 1, s2 2), fp32,
 // raster channel order.  hipErrorNotSupported when the level does not fit a band workgroup
 // (the caller then runs the warp and correlation kernels separately).  `warp` = 0 correlates
