@@ -57,7 +57,23 @@ struct Geo {
   int f1f;   // floats of one chunk's f1 image: ck * R * 2 * Wq4
   int f2f;   // floats of one chunk's f2 image: ck * NR2 * 2 * Wf
   float inv_Q, inv_NR2, inv_I, inv_S, inv_W4;
+  int census;  // measurement only (knob rows_census): phase stamps -> g_rows_census
 };
+
+// Phase timestamps (measurement only): s_memrealtime (100 MHz) of workgroup b's thread 0 as a
+// branch-free buffer store (off unless g.census)
+__device__ unsigned long long g_rows_census[4096 * 8];
+typedef unsigned u32x2c __attribute__((ext_vector_type(2)));
+#define ROWS_MARK(k)                                                                        \
+  do {                                                                                      \
+    const bool on_ = g.census && threadIdx.x == 0 && blockIdx.x < 4096;                     \
+    const unsigned long long ts_ = __builtin_amdgcn_s_memrealtime();                        \
+    __builtin_amdgcn_raw_buffer_store_b64(                                                  \
+        __builtin_bit_cast(u32x2c, ts_),                                                    \
+        __builtin_amdgcn_make_buffer_rsrc((void*)g_rows_census, (short)0,                   \
+                                          (int)sizeof(g_rows_census), 0x00020000),          \
+        on_ ? (int)((blockIdx.x * 8 + (k)) * 8) : (int)0x80000000, 0, 0);                   \
+  } while (0)
 
 __device__ __forceinline__ int qdiv(int x, float inv) {
   return (int)(((float)x + 0.5f) * inv);
@@ -80,6 +96,7 @@ __device__ __forceinline__ void rows_band(const T* __restrict__ f1, const T* __r
   constexpr int EPQ = 16 / (int)sizeof(T);  // pixels per 16-B quad
   constexpr int HPQ = EPQ / 2;              // parity slots per quad and column parity
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  ROWS_MARK(0);
   const int NR2 = g.NR2;
   const int t = threadIdx.x;
   const int tg = unit0 % g.TS, unit = unit0 / g.TS;    // displacement-row group
@@ -201,6 +218,7 @@ __device__ __forceinline__ void rows_band(const T* __restrict__ f1, const T* __r
       if (ld2[j] >= 0) put(ld2[j], g.Wf, v2[j]);
     if (cb + g.ck < C) issue(cb + g.ck);
     lds_barrier();
+    ROWS_MARK(cb == 0 ? 1 : 3);
     if (active) {
       const float* pa = f1s + a_off;
       const float* pb = lds + b_off;
@@ -220,12 +238,14 @@ __device__ __forceinline__ void rows_band(const T* __restrict__ f1, const T* __r
     }
   }
   lds_barrier();  // staging dead: partial sums reuse it
+  ROWS_MARK(4);
   if (active) {
     f32x4* rp = reinterpret_cast<f32x4*>(lds) + (grp * g.I + it) * D;
 #pragma unroll
     for (int ti = 0; ti < D; ++ti) rp[ti] = f32x4{acc[ti][0], acc[ti][1], acc[ti][2], acc[ti][3]};
   }
   lds_barrier();
+  ROWS_MARK(5);
 
   // ---- epilogue: lane = 4 consecutive x of one (tj, ti, row); fixed-order group sum ----
   const int W4 = W >> 2;
@@ -267,6 +287,7 @@ __device__ __forceinline__ void rows_band(const T* __restrict__ f1, const T* __r
     else
       st_out4(dst, v4);
   }
+  ROWS_MARK(6);
 }
 
 template <typename T, int R, int NT, int ML1, int ML2>
@@ -391,6 +412,7 @@ static hipError_t plan(int B, int C, int H, int W, float divisor, int dtype, Pla
   g.inv_I = 1.f / (float)g.I;
   g.inv_S = 1.f / (float)g.S;
   g.inv_W4 = 1.f / (float)(W / 4);
+  g.census = debug_knob("rows_census", 0);
   int ex;
   const float mnt = std::frexp(divisor, &ex);
   const float inv = (mnt == 0.5f) ? std::ldexp(1.f, 1 - ex) : 0.f;
@@ -420,6 +442,15 @@ static hipError_t plan(int B, int C, int H, int W, float divisor, int dtype, Pla
   X(_Float16, 2, 2, 6)                                                       \
   X(_Float16, 1, 1, 3)                                                       \
   X(_Float16, 1, 2, 5)
+
+extern "C" __attribute__((visibility("default"))) int pwc_debug_rows_census(void* dst, int n) {
+  if (dst == nullptr) {
+    static unsigned long long zeros[4096 * 8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(rows::g_rows_census), zeros, sizeof(zeros)) == hipSuccess;
+  }
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(rows::g_rows_census),
+                             sizeof(unsigned long long) * (size_t)n) == hipSuccess;
+}
 
 // Whether corr_forward_rows serves this problem (a plan and an instantiated variant exist).
 bool corr_rows_accepts(int B, int C, int H, int W, int dtype) {
