@@ -322,9 +322,8 @@ class HipPass:
     def grouped_levels(self, s):
         """The fused levels issued as one pwc_warp_corr_forward_group call (>= 2 of them)."""
         lv = sorted(l for l in self.fused if l < len(s) - 1)
-        # the paired kernel is the fp32 band kernel; other dtypes keep per-level calls with
-        # their split-channel workspaces
-        ok = self.group and len(lv) >= 2 and self.dtype == torch.float32
+        # the paired kernel is the band kernel (fp32 or fp16 storage)
+        ok = self.group and len(lv) >= 2
         return lv if ok else []
 
     def warp_levels(self, s):
@@ -885,7 +884,10 @@ def main(argv=None):
         sync()
         ref = p.fresh(s)
         diff = [_diff(lv["corr"], r) for lv, r in zip(s, ref)]
-        ok = all(d <= 1e-5 for d in diff)
+        # fused / grouped levels sum in another order than the unfused recomputation: fp32
+        # within 1e-5, fp16 storage within its output rounding
+        tol = 1e-5 if dtype == torch.float32 else 2e-3
+        ok = all(d <= tol for d in diff)
         if world > 1:
             flag = torch.tensor([int(ok)], device=dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)

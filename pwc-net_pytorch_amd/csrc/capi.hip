@@ -39,10 +39,10 @@ hipError_t corr_forward_rows_pair(const void*, const void*, void*, int, int, int
                                   const void*, const void*, void*, int, int, int, int, float,
                                   float, hipStream_t);
 hipError_t flow_up2_backward_f32(const void*, void*, int, int, int, hipStream_t);
-hipError_t warp_corr_band_pair_f32(const BandProblem& a, const BandProblem& b, float divisor_a,
-                                   float divisor_b, hipStream_t stream);
-hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void*, int, int, int,
-                              int, float, int, hipStream_t);
+hipError_t warp_corr_band_pair(const BandProblem& a, const BandProblem& b, float divisor_a,
+                               float divisor_b, int dtype, hipStream_t stream);
+hipError_t warp_corr_band(const void*, const void*, const void*, void*, void*, int, int, int, int,
+                          float, int, int, hipStream_t);
 }  // namespace pwc
 
 namespace pwc {
@@ -580,8 +580,8 @@ int pwc_flow_upsample_backward(const void* grad_flow_up, void* grad_flow_coarse,
 // then the correlation kernels (x2_warp, or the workspace's tail when x2_warp is NULL, holds
 // the warped features in between).
 static bool warp_corr_fusable(int pad, int k, int md, int s1, int s2, int dtype) {
-  return dtype == PWC_DTYPE_F32 && k == 1 && s1 == 1 && s2 == 2 && pad == md &&
-         (md == 8 || md == 9);
+  return (dtype == PWC_DTYPE_F32 || dtype == PWC_DTYPE_F16) && k == 1 && s1 == 1 && s2 == 2 &&
+         pad == md && (md == 8 || md == 9);
 }
 
 static int fused_disabled() { return pwc::debug_knob("fused", 1) == 0; }
@@ -623,8 +623,8 @@ int pwc_warp_corr_forward(const void* in1, const void* x2, const void* flow, voi
   hipStream_t s = (hipStream_t)stream;
   if (!fused_disabled() && warp_corr_fusable(pad_size, kernel_size, max_displacement, stride1,
                                              stride2, dtype)) {
-    const hipError_t e = pwc::warp_corr_band_f32(in1, x2, flow, x2_warp, out, B, C, H, W,
-                                                 (float)C, 1, s);
+    const hipError_t e = pwc::warp_corr_band(in1, x2, flow, x2_warp, out, B, C, H, W,
+                                             (float)C, 1, dtype, s);
     if (e != hipErrorNotSupported) return check_launch(fn, e);
   }
   // two launches: warp into x2_warp (or the workspace tail), then the correlation
@@ -682,7 +682,7 @@ int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, int count
       const pwc_warp_corr_problem& p = problems[open];
       const pwc::BandProblem a{p.in1, p.x2, p.flow, p.x2_warp, p.out, p.B, p.C, p.H, p.W};
       const pwc::BandProblem b{q.in1, q.x2, q.flow, q.x2_warp, q.out, q.B, q.C, q.H, q.W};
-      const hipError_t e = pwc::warp_corr_band_pair_f32(a, b, (float)p.C, (float)q.C, s);
+      const hipError_t e = pwc::warp_corr_band_pair(a, b, (float)p.C, (float)q.C, dtype, s);
       if (e == hipErrorNotSupported) {
         open = i;  // no pair with the open one: try the next problem against this one
         continue;

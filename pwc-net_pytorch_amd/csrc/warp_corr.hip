@@ -84,28 +84,63 @@ __device__ unsigned long long g_band_dbg[4096 * 8];
   } while (0)
 
 // One problem of a (possibly grouped) launch: the tensors and geometry of one level.
-struct Prob {
-  const float* f1;
-  const float* x2;
-  const float* flow;
-  float* x2w;
-  float* out;
+struct Prob {  // element pointers of the problem's storage type (fp32 or fp16)
+  const void* f1;
+  const void* x2;
+  const void* flow;
+  void* x2w;
+  void* out;
   int C, H, W;
   float divisor, inv_divisor, halfx, halfy;
   Geo g;
 };
 
+// Storage-type loads and stores of the band kernel (fp32, or fp16 with fp32 arithmetic: each
+// element widened on the way into LDS, each result rounded on the way out).
+template <typename E>
+__device__ __forceinline__ float ld_elem(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t so) {
+  if constexpr (sizeof(E) == 4)
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, (int)so, 0));
+  else
+    return to_f32(__builtin_bit_cast(__half, __builtin_amdgcn_raw_buffer_load_b16(rs, (int)off,
+                                                                                   (int)so, 0)));
+}
+// two horizontally adjacent elements (a bilinear corner pair)
+template <typename E>
+__device__ __forceinline__ void ld_pair(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t so,
+                                        float& lo, float& hi) {
+  if constexpr (sizeof(E) == 4) {
+    const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, (int)so, 0);
+    lo = __uint_as_float(a.x);
+    hi = __uint_as_float(a.y);
+  } else {
+    const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, (int)so, 0);
+    lo = to_f32(__builtin_bit_cast(__half, (unsigned short)(a & 0xffffu)));
+    hi = to_f32(__builtin_bit_cast(__half, (unsigned short)(a >> 16)));
+  }
+}
+template <typename E>
+__device__ __forceinline__ void st_elem_nt(float v, __amdgpu_buffer_rsrc_t rs, uint32_t off,
+                                           uint32_t so) {
+  if constexpr (sizeof(E) == 4)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)off, (int)so, 2 /* nt */);
+  else
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, from_f32<__half>(v)),
+                                          rs, (int)off, (int)so, 2 /* nt */);
+}
+
 // The workgroup body; `bid` is the workgroup's index inside its problem's grid.  MJ: channels
 // per staging batch per thread (loads in flight; MAXJ for the single-level kernel, 16 under
 // the two-workgroups-per-CU register cap of the grouped kernel).
-template <int R, int T, bool WARP, int MJ>
+template <typename E, int R, int T, bool WARP, int MJ>
 __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds, const Prob& P,
                                           const OutEpi& epi) {
-  const float* __restrict__ f1 = P.f1;
-  const float* __restrict__ x2 = P.x2;
-  const float* __restrict__ flow = P.flow;
-  float* __restrict__ x2w = P.x2w;
-  float* __restrict__ out = P.out;
+  constexpr uint32_t ES = (uint32_t)sizeof(E);
+  const E* __restrict__ f1 = (const E*)P.f1;
+  const E* __restrict__ x2 = (const E*)P.x2;
+  const E* __restrict__ flow = (const E*)P.flow;
+  E* __restrict__ x2w = (E*)P.x2w;
+  E* __restrict__ out = (E*)P.out;
   const int C = P.C, H = P.H, W = P.W;
   const float divisor = P.divisor, inv_divisor = P.inv_divisor, halfx = P.halfx,
               halfy = P.halfy;
@@ -135,13 +170,13 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
   // load of a thread is issued before anything waits: flow and f1 first, the LDS clear runs
   // under them, then the bilinear gathers. ----
   constexpr uint32_t kOOB = 0x80000000u;
-  const uint32_t img_bytes = (uint32_t)C * plane * 4u;
+  const uint32_t img_bytes = (uint32_t)C * plane * ES;
   const int np1 = R * W, ncg1 = NT / np1;
   const int cg1 = qdiv(t, g.inv_np1), pix1 = t - cg1 * np1;
   const int r1 = qdiv(pix1, g.inv_W), x1 = pix1 - r1 * W;
   const bool ok1 = cg1 < ncg1 && r0 + r1 < hp && !(g.abl & 1);
   const uint32_t vo1 =
-      ok1 ? ((uint32_t)cg1 * plane + (uint32_t)(2 * (r0 + r1) + p) * W + x1) * 4u : kOOB;
+      ok1 ? ((uint32_t)cg1 * plane + (uint32_t)(2 * (r0 + r1) + p) * W + x1) * ES : kOOB;
   const int dst1 = (r1 * 2 + (x1 & 1)) * g.Wq4 + (x1 >> 1);
 
   const int np2 = NR2 * W, ncg2 = NT / np2;
@@ -156,7 +191,7 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
   const bool emit = WARP && ok2 && x2w != nullptr && tj0 <= 4 && 4 < tj0 + T &&
                     k2 >= 4 - tj0 && k2 < 4 - tj0 + R;
   const uint32_t cbase2 = (uint32_t)cg2 * plane;
-  const uint32_t vow = emit ? (cbase2 + src2) * 4u : kOOB;
+  const uint32_t vow = emit ? (cbase2 + src2) * ES : kOOB;
   const size_t img = (size_t)n * C * plane;
   const __amdgpu_buffer_rsrc_t rs1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(f1 + img), (short)0, (int)img_bytes, 0x00020000);
@@ -164,13 +199,13 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
       __builtin_amdgcn_make_buffer_rsrc((void*)(x2 + img), (short)0, (int)img_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(x2w ? x2w + img : x2w), (short)0, x2w ? (int)img_bytes : 0, 0x00020000);
-  const uint32_t cs1 = (uint32_t)ncg1 * plane * 4u;  // bytes between a thread's channels
-  const uint32_t cs2 = (uint32_t)ncg2 * plane * 4u;
+  const uint32_t cs1 = (uint32_t)ncg1 * plane * ES;  // bytes between a thread's channels
+  const uint32_t cs2 = (uint32_t)ncg2 * plane * ES;
 
   float fu = 0.f, fv = 0.f;
   if constexpr (WARP) {
-    fu = flow[(unsigned)(2 * n + 0) * plane + src2];
-    fv = flow[(unsigned)(2 * n + 1) * plane + src2];
+    fu = to_f32(flow[(unsigned)(2 * n + 0) * plane + src2]);
+    fv = to_f32(flow[(unsigned)(2 * n + 1) * plane + src2]);
   }
   // channels per thread (uniform): iterations past it are skipped by a scalar branch
   const int nj1 = (C + ncg1 - 1) / ncg1, nj2 = (C + ncg2 - 1) / ncg2;
@@ -180,8 +215,7 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
       if (jb1 + j >= nj1) break;
-      v1[j] = __uint_as_float(
-          __builtin_amdgcn_raw_buffer_load_b32(rs1, (int)vo1, (int)((jb1 + j) * cs1), 0));
+      v1[j] = ld_elem<E>(rs1, vo1, (uint32_t)((jb1 + j) * cs1));
     }
   };
   auto f1_store = [&]() {
@@ -214,23 +248,19 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
     w11 = bl.wx1 * bl.wy1;
     kp = pairs(bl, H, W);  // W >= 2 (launcher)
   }
-  const uint32_t voA = ok2 ? (cbase2 + (WARP ? kp.i0 : src2)) * 4u : kOOB;
-  const uint32_t voB = ok2 ? (cbase2 + kp.i1) * 4u : kOOB;
+  const uint32_t voA = ok2 ? (cbase2 + (WARP ? kp.i0 : src2)) * ES : kOOB;
+  const uint32_t voB = ok2 ? (cbase2 + kp.i1) * ES : kOOB;
   float lo[MJ][2], hi[MJ][2];
   auto f2_issue = [&]() {
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
       if (jb2 + j >= nj2) break;
-      const int so = (int)((jb2 + j) * cs2);
+      const uint32_t so = (uint32_t)((jb2 + j) * cs2);
       if constexpr (WARP) {
-        const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(rs2, (int)voA, so, 0);
-        const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(rs2, (int)voB, so, 0);
-        lo[j][0] = __uint_as_float(a.x);
-        hi[j][0] = __uint_as_float(a.y);
-        lo[j][1] = __uint_as_float(b.x);
-        hi[j][1] = __uint_as_float(b.y);
+        ld_pair<E>(rs2, voA, so, lo[j][0], hi[j][0]);
+        ld_pair<E>(rs2, voB, so, lo[j][1], hi[j][1]);
       } else {
-        lo[j][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs2, (int)voA, so, 0));
+        lo[j][0] = ld_elem<E>(rs2, voA, so);
       }
     }
   };
@@ -253,6 +283,9 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
         acc = fmaf(masked(c01, kp.m01), w01, acc);
         acc = fmaf(masked(c10, kp.m10), w10, acc);
         acc = fmaf(masked(c11, kp.m11), w11, acc);
+        // fp16 storage: the correlation reads x2_warp as stored (rounded), as the two-launch
+        // path does
+        if constexpr (ES == 2) acc = to_f32(from_f32<__half>(acc));
         val = acc;
         lo[j][0] = acc;
       } else {
@@ -264,8 +297,7 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
 #pragma unroll
       for (int j = 0; j < MJ; ++j) {
         if (jb2 + j >= nj2) break;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lo[j][0]), rsw, (int)vow,
-                                              (int)((jb2 + j) * cs2), 2 /* nt */);
+        st_elem_nt<E>(lo[j][0], rsw, vow, (uint32_t)((jb2 + j) * cs2));
       }
     }
   };
@@ -361,8 +393,11 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
     float sum = (s0 + s1) + (s2 + s3);
     sum = inv_divisor != 0.f ? sum * inv_divisor : sum / divisor;
     const size_t ib = epi.ostride ? (size_t)n * epi.ostride : (size_t)n * (D * D) * H * W;
-    st_out1(out + ib + ((size_t)(tj * D + ti) * H + (2 * row + p)) * W + x,
-            epi_act(sum, epi.slope));
+    E* dst = out + ib + ((size_t)(tj * D + ti) * H + (2 * row + p)) * W + x;
+    if constexpr (ES == 4)
+      st_out1(reinterpret_cast<float*>(dst), epi_act(sum, epi.slope));
+    else
+      *dst = from_f32<E>(epi_act(sum, epi.slope));
   }
   if (g.abl & 256) {
     __syncthreads();
@@ -370,10 +405,10 @@ __device__ __forceinline__ void band_body(const int bid, float* __restrict__ lds
   }
 }
 
-template <int R, int T, bool WARP>
+template <typename E, int R, int T, bool WARP>
 __global__ __launch_bounds__(NT, 1) void warp_corr_band(Prob P, OutEpi epi) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  band_body<R, T, WARP, MAXJ>((int)blockIdx.x, lds, P, epi);
+  band_body<E, R, T, WARP, MAXJ>((int)blockIdx.x, lds, P, epi);
 }
 
 // Two independent problems in one launch (e.g. two coarse levels, or two requests): blocks
@@ -381,14 +416,14 @@ __global__ __launch_bounds__(NT, 1) void warp_corr_band(Prob P, OutEpi epi) {
 // grids holds its CU for a few microseconds at two waves per SIMD, so the two grids co-reside
 // (<= 128 VGPRs: two 512-thread workgroups per CU; the launcher checks that the two LDS
 // footprints fit one CU together) instead of running one after the other.
-template <int R0, int T0, int R1, int T1>
+template <typename E, int R0, int T0, int R1, int T1>
 __global__ __launch_bounds__(NT, 2) void warp_corr_band_pair(Prob P0, Prob P1, int nblk0,
                                                              OutEpi epi) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if ((int)blockIdx.x < nblk0)
-    band_body<R0, T0, true, 16>((int)blockIdx.x, lds, P0, epi);
+    band_body<E, R0, T0, true, 16>((int)blockIdx.x, lds, P0, epi);
   else
-    band_body<R1, T1, true, 16>((int)blockIdx.x - nblk0, lds, P1, epi);
+    band_body<E, R1, T1, true, 16>((int)blockIdx.x - nblk0, lds, P1, epi);
 }
 
 struct Cfg {
@@ -406,19 +441,20 @@ static bool env_cfg(int* R, int* T, int* G) {
   return true;
 }
 
-template <int R, int T, bool WARP>
+template <typename E, int R, int T, bool WARP>
 static hipError_t launch(const Prob& P, size_t lds, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&warp_corr_band<R, T, WARP>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&warp_corr_band<E, R, T, WARP>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int ntg = (D + T - 1) / T;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);
-  hipExtLaunchKernelGGL((warp_corr_band<R, T, WARP>), dim3((unsigned)(P.g.units * ntg)),
+  hipExtLaunchKernelGGL((warp_corr_band<E, R, T, WARP>), dim3((unsigned)(P.g.units * ntg)),
                         dim3(NT), lds, stream, ev0, ev1, 0, P, current_epi());
   return hipGetLastError();
 }
@@ -495,12 +531,15 @@ static bool make_prob(const void* f1, const void* x2, const void* flow, void* x2
       *T = 3;
     }
   }
+  // a level whose all-channel staging exceeds the LDS runs as two launches (config-4 Sintel l1,
+  // 128 channels x 32 columns: a lower band measured 2x slower than warp + row-band
+  // correlation, profiles/r03e_band_fp16.txt)
   if (!make_geo(B, C, H, W, *R, *T, Greq, &P->g, lds)) return false;
-  P->f1 = (const float*)f1;
-  P->x2 = (const float*)x2;
-  P->flow = (const float*)flow;
-  P->x2w = (float*)x2w;
-  P->out = (float*)out;
+  P->f1 = f1;
+  P->x2 = x2;
+  P->flow = flow;
+  P->x2w = x2w;
+  P->out = out;
   P->C = C;
   P->H = H;
   P->W = W;
@@ -525,15 +564,16 @@ bool warp_corr_band_accepts(int B, int C, int H, int W, int warp) {
                          &R, &T, &P, &lds);
 }
 
-// Fused warp -> correlation for Correlation(pad == md in {8, 9}, k 1, s1 1, s2 2), fp32,
-// raster channel order.  hipErrorNotSupported when the level does not fit a band workgroup
-// (the caller then runs the warp and correlation kernels separately).  `warp` = 0 correlates
-// x2 directly (flow and x2w unused).
-hipError_t warp_corr_band_f32(const void* f1, const void* x2, const void* flow, void* x2w,
-                              void* out, int B, int C, int H, int W, float divisor, int warp,
-                              hipStream_t stream) {
+// Fused warp -> correlation for Correlation(pad == md in {8, 9}, k 1, s1 1, s2 2), fp32 or fp16
+// storage (dtype 0 / 1), raster channel order.  hipErrorNotSupported when the level does not fit
+// a band workgroup (the caller then runs the warp and correlation kernels separately).
+// `warp` = 0 correlates x2 directly (flow and x2w unused).
+hipError_t warp_corr_band(const void* f1, const void* x2, const void* flow, void* x2w, void* out,
+                          int B, int C, int H, int W, float divisor, int warp, int dtype,
+                          hipStream_t stream) {
   using namespace band;
   if (B == 0 || C == 0 || H == 0 || W == 0) return hipSuccess;
+  if (dtype != 0 && dtype != 1) return hipErrorNotSupported;
   if (W < 2 || (size_t)B * C * H * W >= (1ull << 31) || (size_t)B * 81 * H * W >= (1ull << 31))
     return hipErrorNotSupported;
   int R = 0, T = 1;
@@ -541,30 +581,46 @@ hipError_t warp_corr_band_f32(const void* f1, const void* x2, const void* flow, 
   size_t lds;
   if (!make_prob(f1, x2, flow, x2w, out, B, C, H, W, divisor, warp, &R, &T, &P, &lds))
     return hipErrorNotSupported;
+#define PWC_BAND32(RR, TT)                                                                   \
+  if (R == RR && T == TT && dtype == 0)                                                      \
+    return warp ? launch<float, RR, TT, true>(P, lds, stream)                                \
+                : launch<float, RR, TT, false>(P, lds, stream);
 #define PWC_BAND(RR, TT)                                                                     \
-  if (R == RR && T == TT)                                                                    \
-    return warp ? launch<RR, TT, true>(P, lds, stream) : launch<RR, TT, false>(P, lds, stream);
+  if (R == RR && T == TT && dtype == 1)                                                      \
+    return warp ? launch<__half, RR, TT, true>(P, lds, stream)                               \
+                : launch<__half, RR, TT, false>(P, lds, stream);                             \
+  PWC_BAND32(RR, TT)
+  // the per-level choices of make_prob (and its lower-band fallbacks) in both storage types;
+  // two more fp32 shapes the band tests force through the band_r / band_t knobs
   PWC_BAND(3, 1)
-  PWC_BAND(6, 1)
-  PWC_BAND(4, 1)
   PWC_BAND(2, 1)
+  PWC_BAND(1, 1)
   PWC_BAND(2, 3)
-  PWC_BAND(4, 3)
   PWC_BAND(3, 3)
-  PWC_BAND(6, 3)
+  PWC_BAND(1, 3)
+  PWC_BAND32(4, 3)
+  PWC_BAND32(6, 1)
 #undef PWC_BAND
+#undef PWC_BAND32
   return hipErrorNotSupported;
+}
+
+hipError_t warp_corr_band_f32(const void* f1, const void* x2, const void* flow, void* x2w,
+                              void* out, int B, int C, int H, int W, float divisor, int warp,
+                              hipStream_t stream) {
+  return warp_corr_band(f1, x2, flow, x2w, out, B, C, H, W, divisor, warp, 0, stream);
 }
 
 // Two fused warp -> correlation problems (warp = 1, fp32, raster) in ONE launch
 // (warp_corr_band_pair); hipErrorNotSupported when either does not take a band workgroup, their
 // (R, T) pair has no instantiation, or their LDS footprints do not fit one CU together -- the
 // caller then launches them one after the other.
-hipError_t warp_corr_band_pair_f32(const BandProblem& a, const BandProblem& b, float divisor_a,
-                                   float divisor_b, hipStream_t stream) {
+hipError_t warp_corr_band_pair(const BandProblem& a, const BandProblem& b, float divisor_a,
+                               float divisor_b, int dtype, hipStream_t stream) {
   using namespace band;
   if (debug_knob("band_pair", 1) == 0 || !epi_is_default(current_epi()))
     return hipErrorNotSupported;
+  if (dtype != 0 && dtype != 1) return hipErrorNotSupported;
   for (const BandProblem* q : {&a, &b})
     if (q->B == 0 || q->C == 0 || q->H == 0 || q->W == 0) return hipErrorNotSupported;
   int R0 = 0, T0 = 1, R1 = 0, T1 = 1;
@@ -581,25 +637,37 @@ hipError_t warp_corr_band_pair_f32(const BandProblem& a, const BandProblem& b, f
   const int n0 = P0.g.units * ((D + T0 - 1) / T0);
   const int n1 = P1.g.units * ((D + T1 - 1) / T1);
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-#define PWC_PAIR(A0, B0, A1, B1)                                                              \
-  if (R0 == A0 && T0 == B0 && R1 == A1 && T1 == B1) {                                         \
+#define PWC_PAIR_E(E, A0, B0, A1, B1)                                                         \
+  {                                                                                           \
     static bool attr = false;                                                                 \
     if (!attr) {                                                                              \
       hipError_t e = hipFuncSetAttribute(                                                     \
-          reinterpret_cast<const void*>(&warp_corr_band_pair<A0, B0, A1, B1>),                \
+          reinterpret_cast<const void*>(&warp_corr_band_pair<E, A0, B0, A1, B1>),             \
           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
       if (e != hipSuccess) return e;                                                          \
       attr = true;                                                                            \
     }                                                                                         \
     take_launch_events(&ev0, &ev1);                                                           \
-    hipExtLaunchKernelGGL((warp_corr_band_pair<A0, B0, A1, B1>), dim3((unsigned)(n0 + n1)),   \
-                          dim3(NT), lds, stream, ev0, ev1, 0, P0, P1, n0, current_epi());     \
+    hipExtLaunchKernelGGL((warp_corr_band_pair<E, A0, B0, A1, B1>),                           \
+                          dim3((unsigned)(n0 + n1)), dim3(NT), lds, stream, ev0, ev1, 0, P0,  \
+                          P1, n0, current_epi());                                             \
     return hipGetLastError();                                                                 \
+  }
+#define PWC_PAIR(A0, B0, A1, B1)                                                              \
+  if (R0 == A0 && T0 == B0 && R1 == A1 && T1 == B1) {                                         \
+    if (dtype == 1) PWC_PAIR_E(__half, A0, B0, A1, B1)                                        \
+    PWC_PAIR_E(float, A0, B0, A1, B1)                                                         \
   }
   PWC_PAIR(3, 1, 2, 3)  // PWC-Net l0 + l1 (384 x 448: 6 x 7 and 12 x 14)
   PWC_PAIR(2, 3, 3, 1)
 #undef PWC_PAIR
+#undef PWC_PAIR_E
   return hipErrorNotSupported;
+}
+
+hipError_t warp_corr_band_pair_f32(const BandProblem& a, const BandProblem& b, float divisor_a,
+                                   float divisor_b, hipStream_t stream) {
+  return warp_corr_band_pair(a, b, divisor_a, divisor_b, 0, stream);
 }
 
 }  // namespace pwc

@@ -117,3 +117,45 @@ def test_sintel_stream_fp16_channel_pairs(shape, md, s2):
     ref = O.corr_forward(_np(a), _np(b), md, 1, md, 1, s2)
     _close_rel(_np(out), ref, 2e-3)
     _close_rel(_np(single), ref, 2e-3)
+
+
+@pytest.mark.parametrize("shape", SINTEL[:2] + [(2, 192, 6, 7), (2, 128, 12, 14), (1, 24, 13, 15)],
+                         ids=lambda s: "B{}C{}_{}x{}".format(*s))
+def test_fused_band_fp16_coarse_levels(shape):
+    """fp16 WarpCorrelation at the coarse levels runs as ONE band launch (model.py:80-83): its
+    x2_warp equals the fp16 warp kernel's bit for bit (same fmaf chain, same rounding), the
+    correlation reads x2_warp as stored (rounded to fp16, as the two-launch path does), and the
+    volume matches the two-launch path (PWC_DEBUG fused=0) and the oracle on the fp16-rounded
+    warp within the fp16 output rounding."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import warp_corr_forward, warp_forward
+    B, C, H, W = shape
+    rng = np.random.default_rng(60 + H)
+    a, b = _h(rng, *shape), _h(rng, *shape)
+    f = _h(rng, B, 2, H, W, scale=2.0)
+    out, x2w = warp_corr_forward(a, b, f, 9, 1, 9, 1, 2)
+    _lib.set_debug("fused=0")
+    try:
+        out2, x2w2 = warp_corr_forward(a, b, f, 9, 1, 9, 1, 2)
+    finally:
+        _lib.set_debug("")
+    torch.cuda.synchronize()
+    assert out.dtype == torch.float16 and x2w.dtype == torch.float16
+    assert torch.equal(x2w, warp_forward(b, f)) and torch.equal(x2w, x2w2)
+    _close_rel(_np(out), _np(out2), 2e-3)
+    _close_rel(_np(out), O.corr_forward(_np(a), _np(x2w), 9, 1, 9, 1, 2), 2e-3)
+
+
+def test_fused_band_fp16_group_pair_equals_single_calls():
+    """Config 4's l0 + l1 as one paired launch (pwc_warp_corr_forward_group) equal their
+    single-level fused calls bit for bit."""
+    from pwcnet_amd.ops import warp_corr_forward, warp_corr_forward_group
+    rng = np.random.default_rng(71)
+    probs = []
+    for (B, C, H, W) in SINTEL[:2]:
+        probs.append((_h(rng, 4, C, H, W), _h(rng, 4, C, H, W), _h(rng, 4, 2, H, W, scale=2.0)))
+    grouped = warp_corr_forward_group(probs, 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    for (a, b, f), (c, w) in zip(probs, grouped):
+        c1, w1 = warp_corr_forward(a, b, f, 9, 1, 9, 1, 2)
+        assert torch.equal(c, c1) and torch.equal(w, w1)

@@ -135,8 +135,10 @@ def test_fused_md8(md):
 @pytest.mark.parametrize("params", [(4, 1, 4, 1, 1), (9, 1, 9, 1, 2), (3, 3, 2, 1, 1)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 def test_fused_fallback_configs(params, dtype):
-    """Configurations / dtypes the band kernel does not cover run warp + correlation; the
-    result equals the two ops called separately (bitwise: same kernels)."""
+    """Configurations the band kernel does not cover run warp + correlation; the result equals
+    the two ops called separately (bitwise: same kernels).  model.py:24's configuration takes
+    the band kernel in fp32 and fp16 (another summation order: within 1e-5, or the fp16 output
+    rounding); x2_warp is bit-identical either way."""
     from pwcnet_amd.ops import corr_forward, warp_corr_forward, warp_forward
     a, b, f = _inputs(10, 2, 16, 20, 24)
     A, Bt, F = _t(a, dtype), _t(b, dtype), _t(f, dtype)
@@ -146,6 +148,9 @@ def test_fused_fallback_configs(params, dtype):
         ref = corr_forward(A, w, *params)
         if dtype == torch.float32 and params == (9, 1, 9, 1, 2):
             torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+        elif params == (9, 1, 9, 1, 2):
+            err = (out.float() - ref.float()).abs().max() / ref.float().abs().max()
+            assert float(err) <= 2e-3
         else:
             assert torch.equal(out, ref)
         if emit:
