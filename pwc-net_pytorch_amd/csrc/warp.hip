@@ -564,6 +564,9 @@ __global__ __launch_bounds__(256) void warp_bwd_far(const float* __restrict__ fl
                                                     float* __restrict__ gx, int B, int C, int H,
                                                     int W, float halfx, float halfy, int th,
                                                     int tw) {
+  // grid.y = groups of 8 channels: a far pixel's channels are spread over workgroups, and each
+  // thread issues its 8 grad_out loads before its atomics (a load -> atomic chain per channel
+  // made this pass's tail: up to 50 us at C = 96, one thread doing every channel)
   const unsigned plane = (unsigned)(H * W);
   const unsigned idx = blockIdx.x * 256u + threadIdx.x;
   if (idx >= (unsigned)B * plane) return;
@@ -580,13 +583,19 @@ __global__ __launch_bounds__(256) void warp_bwd_far(const float* __restrict__ fl
   if (!(o00 || o01 || o10 || o11)) return;
   const float w00 = b.wx0 * b.wy0, w01 = b.wx1 * b.wy0;
   const float w10 = b.wx0 * b.wy1, w11 = b.wx1 * b.wy1;
-  for (int c = 0; c < C; ++c) {
-    const float g = gout[((unsigned)(n * C + c)) * plane + pix];
-    float* q = gx + ((unsigned)(n * C + c)) * plane;
-    if (o00) atomicAdd(q + k.i00, g * w00);
-    if (o01) atomicAdd(q + k.i01, g * w01);
-    if (o10) atomicAdd(q + k.i10, g * w10);
-    if (o11) atomicAdd(q + k.i11, g * w11);
+  const int c0 = (int)blockIdx.y * 8;
+  float g[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    g[i] = c0 + i < C ? gout[((unsigned)(n * C + c0 + i)) * plane + pix] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (c0 + i >= C) break;
+    float* q = gx + ((unsigned)(n * C + c0 + i)) * plane;
+    if (o00) atomicAdd(q + k.i00, g[i] * w00);
+    if (o01) atomicAdd(q + k.i01, g[i] * w01);
+    if (o10) atomicAdd(q + k.i10, g[i] * w10);
+    if (o11) atomicAdd(q + k.i11, g[i] * w11);
   }
 }
 
@@ -740,9 +749,10 @@ hipError_t warp_backward_f32(const void* x, const void* flow, const void* gout, 
       if (done) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(warp_bwd_far, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0,
-                           stream, (const float*)flow, (const float*)gout, (float*)gx, B, C, H,
-                           W, halfx, halfy, THm, TWm);
+        hipLaunchKernelGGL(warp_bwd_far,
+                           dim3((unsigned)((npix + 255) / 256), (unsigned)((C + 7) / 8)),
+                           dim3(256), 0, stream, (const float*)flow, (const float*)gout,
+                           (float*)gx, B, C, H, W, halfx, halfy, THm, TWm);
         return hipGetLastError();
       }
     }

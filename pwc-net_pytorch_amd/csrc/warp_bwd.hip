@@ -417,26 +417,32 @@ __global__ __launch_bounds__(256) void warp_bwd_finish(Args a) {
     a.gflow[(size_t)(2 * n) * plane + pix] = (sx * mx) / a.halfx;
     a.gflow[(size_t)(2 * n + 1) * plane + pix] = (sy * my) / a.halfy;
   }
-  // far corners: block b takes the waves' lists of tile workgroups b, b + gridDim.x, ...
-  for (int wg = blockIdx.x; wg < a.nwg; wg += gridDim.x) {
-    for (int v = 0; v < NT / 64; ++v) {
-      const unsigned nf = a.farcnt[(size_t)wg * (NT / 64) + v];
-      const unsigned* lst = a.far + ((size_t)wg * (NT / 64) + v) * 256;
-      for (unsigned e = threadIdx.x; e < nf; e += blockDim.x) {
-        const unsigned code = lst[e];
-        const int k = (int)(code & 3u);
-        const unsigned gp = code >> 2, nn = gp / plane, pix = gp - nn * plane;
-        const int py = (int)(pix / (unsigned)W), px = (int)pix - py * W;
-        const float* fn = a.flow + (size_t)(2 * nn) * plane;
-        const Bilinear b = bilinear(src_coord(fn[pix], px, W, a.halfx),
-                                    src_coord(fn[plane + pix], py, H, a.halfy), H, W);
-        const int cy = b.y0 + (k >> 1), cx = b.x0 + (k & 1);
-        const float w = corner_w(b, k);
-        const unsigned q = (unsigned)(cy * W + cx);
-        for (int c = 0; c < C; ++c) {
-          const size_t o = ((size_t)nn * C + c) * plane;
-          atomicAdd(a.gx + o + q, a.gout[o + pix] * w);
-        }
+  // far corners: block b takes the 8 wave lists of tile workgroups b, b + gridDim.x, ...; 32
+  // threads per list, every count loaded at once (a per-list load -> loop chain made this
+  // kernel's tail)
+  const int nl = NT / 64, v = threadIdx.x >> 5, tl = threadIdx.x & 31;
+  for (int wg = blockIdx.x; wg < a.nwg && v < nl; wg += gridDim.x) {
+    const unsigned nf = a.farcnt[(size_t)wg * nl + v];
+    const unsigned* lst = a.far + ((size_t)wg * nl + v) * 256;
+    for (unsigned e = tl; e < nf; e += 32) {
+      const unsigned code = lst[e];
+      const int k = (int)(code & 3u);
+      const unsigned gp = code >> 2, nn = gp / plane, pix = gp - nn * plane;
+      const int py = (int)(pix / (unsigned)W), px = (int)pix - py * W;
+      const float* fn = a.flow + (size_t)(2 * nn) * plane;
+      const Bilinear b = bilinear(src_coord(fn[pix], px, W, a.halfx),
+                                  src_coord(fn[plane + pix], py, H, a.halfy), H, W);
+      const int cy = b.y0 + (k >> 1), cx = b.x0 + (k & 1);
+      const float w = corner_w(b, k);
+      const unsigned q = (unsigned)(cy * W + cx);
+      for (int c0 = 0; c0 < C; c0 += 8) {  // 8 loads in flight, then their atomics
+        float g[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          g[i] = c0 + i < C ? a.gout[((size_t)nn * C + c0 + i) * plane + pix] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (c0 + i < C) atomicAdd(a.gx + ((size_t)nn * C + c0 + i) * plane + q, g[i] * w);
       }
     }
   }
