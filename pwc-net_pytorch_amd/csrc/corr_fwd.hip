@@ -394,7 +394,17 @@ hipError_t corr_reduce_splits_f32(const void* partial, void* out, size_t n, int 
   return corr_reduce_splits_t<float>(partial, out, n, nsplit, divisor, stream);
 }
 
-int corr_pick_splits(long long base_blocks, int nchunks, int max_splits);  // corr_ring.hip
+// Channel splits for a grid of `base_blocks` workgroups: none once the grid alone gives every
+// CU a workgroup; otherwise aim at two workgroups per CU (512), at most one split per channel
+// chunk and at most `max_splits` (the caller sizes max_splits so that the partial volumes stay
+// within the workspace budget, corr_workspace_bytes).
+static int corr_pick_splits(long long base_blocks, int nchunks, int max_splits) {
+  if (base_blocks <= 0 || base_blocks >= 256) return 1;
+  long long k = (512 + base_blocks - 1) / base_blocks;
+  if (k > nchunks) k = nchunks;
+  if (k > max_splits) k = max_splits;
+  return k < 1 ? 1 : (int)k;
+}
 
 // ------------------------------------------------------------------------------------
 // host-side launchers
@@ -460,12 +470,6 @@ static hipError_t launch_generic(const void* in1, const void* in2, void* out, in
   return hipGetLastError();
 }
 
-// corr_ring.hip
-hipError_t corr_forward_ring_f32(const void* in1, const void* in2, void* out, int B, int C,
-                                 int H, int W, int Ho, int Wo, int off, int dr, int s2,
-                                 int layout, float divisor, int max_splits, void* partial,
-                                 hipStream_t stream);
-
 // corr_pt.hip
 hipError_t corr_forward_pt_f32(const void* in1, const void* in2, void* out, int B, int C, int H,
                                int W, int Ho, int Wo, int off, int dr, int s2, int layout,
@@ -476,11 +480,6 @@ hipError_t corr_forward_small_f32(const void* in1, const void* in2, void* out, i
                                   int H, int W, int Ho, int Wo, int off, int dr, int s2,
                                   int layout, float divisor, int max_splits, void* partial,
                                   hipStream_t stream);
-
-// corr_grp.hip
-hipError_t corr_forward_grp_f32(const void* in1, const void* in2, void* out, int B, int C, int H,
-                                int W, int Ho, int Wo, int off, int dr, int s2, int layout,
-                                float divisor, hipStream_t stream);
 
 // Channel-split budget: nsplit partial volumes of B*OC*Ho*Wo floats, nsplit <= kMaxSplits and
 // nsplit * volume <= kSplitBudget; no workspace once the 16x16 tiles alone fill the chip.
@@ -505,9 +504,8 @@ static bool pt_disabled() { return debug_knob("corr_pt", 1) == 0; }
 
 // The band kernel of warp_corr.hip (without the warp) serves model.py:24's correlation at the
 // smallest levels (parity half of <= 6 rows: l0, l1 at 384x448; measured 6.8 / 7.8 us against
-// 11.0 / 13.4 us for corr_small + its reduce).  Knob corr_band=0 disables it, =2 forces it at
-// every size (measurement).
-static int band_mode() { return debug_knob("corr_band", 1); }
+// 11.0 / 13.4 us for corr_small + its reduce).  Knob corr_band=0 disables it (measurement).
+static bool band_enabled() { return debug_knob("corr_band", 1) != 0; }
 
 hipError_t warp_corr_band_f32(const void*, const void*, const void*, void*, void*, int, int, int,
                               int, float, int, hipStream_t);
@@ -534,7 +532,7 @@ int corr_forward_path(const void* in1, const void* in2, const void* out, int B, 
       corr_stream_accepts(in1, in2, out, B, C, H, W, s2, half ? 1 : 0))
     return kPathStream;
   const bool c9 = layout == kRaster && s2 == 2 && pad == md && (md == 8 || md == 9);
-  if (c9 && dtype == 0 && (band_mode() == 2 || (band_mode() == 1 && (H + 1) / 2 <= 6)) &&
+  if (c9 && dtype == 0 && band_enabled() && (H + 1) / 2 <= 6 &&
       warp_corr_band_accepts(B, C, H, W, 0))
     return kPathBand;
   if (c9 && (dtype == 0 || half) && (uintptr_t)in1 % 16 == 0 && (uintptr_t)in2 % 16 == 0 &&
@@ -544,9 +542,6 @@ int corr_forward_path(const void* in1, const void* in2, const void* out, int B, 
 }
 
 // corr_rows.hip (row bands over full rows) serves l3-sized grids (it decides; PWC_ROWS).
-
-// knob corr_grp=0 disables the coarse-level kernel (measurement of the split path only).
-static bool grp_disabled() { return debug_knob("corr_grp", 1) == 0; }
 
 // `workspace` (>= corr_workspace_bytes) enables channel splitting for grids too small to fill
 // the chip; null keeps one workgroup per tile over all channels.
@@ -561,7 +556,7 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
   const int max_splits = workspace ? corr_max_splits(B, D * D, Ho, Wo) : 1;
   if (max_splits <= 1) workspace = nullptr;
   // a strided / activated output (pwc_corr_forward_into) is written by the band, row-band,
-  // parity-tile and ring kernels only; every other path declines before launching
+  // parity-tile and stream kernels only; every other path declines before launching
   const bool epi_def = epi_is_default(current_epi());
   constexpr bool kHalf = std::is_same<T, __half>::value;
   const int path = force_generic == 0 && (sizeof(T) == 4 || kHalf)
@@ -592,19 +587,6 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
                                                   workspace, stream);
       if (e != hipErrorNotSupported) return e;
     }
-    // coarse levels (too few 16x16 tiles to fill the chip) with 16-B aligned rows:
-    // in-workgroup channel groups (corr_grp.hip); unaligned rows (W % 4 != 0, the smallest
-    // pyramid levels) measured faster on the channel-split path below.
-    const long long tiles = (long long)B * ((Ho + 15) / 16) * ((Wo + 15) / 16);
-    if (tiles < 256 && W % 4 == 0 && (md - pad) % 4 == 0 && !grp_disabled() && epi_def) {
-      const hipError_t e = corr_forward_grp_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad,
-                                                dr, s2, layout, divisor, stream);
-      if (e != hipErrorNotSupported) return e;
-    }
-    const hipError_t e = corr_forward_ring_f32(in1, in2, out, B, C, H, W, Ho, Wo, md - pad, dr,
-                                               s2, layout, divisor, max_splits, workspace,
-                                               stream);
-    if (e != hipErrorNotSupported) return e;
   }
   if (!epi_def) return hipErrorNotSupported;
   if (force_generic != 1 && k == 1 && s1 == 1 && dr == 4) {

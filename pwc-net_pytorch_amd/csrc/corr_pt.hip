@@ -439,16 +439,14 @@ hipError_t corr_forward_pt_f32(const void* in1, const void* in2, void* out, int 
   if (const int k = debug_knob("pt_k", 0)) groups = k;
   if (groups <= 0) {
     // the largest tile (fewest halo bytes per output) that still gives ~one tile per CU;
-    // grids that fill the chip with single-group tiles stay on corr_ring.hip (measured equal
-    // or faster at l4 inside the bench's graph, where the warp has just written input2)
+    // grids that fill the chip with single-group tiles (l4-sized, when the stream and row-band
+    // kernels decline the shape) take Pt1
     const int hp = (Ho + 1) / 2, ntx = (Wo + 15) / 16;
     groups = 8;
     for (int k : {1, 2, 4}) {
       const long long tiles = (long long)B * 2 * ((hp + 24 / k - 1) / (24 / k)) * ntx;
       if (tiles >= 192) { groups = k; break; }
     }
-    const bool l4 = debug_knob("pt_l4", 0) == 1;
-    if (groups == 1 && !l4) return hipErrorNotSupported;
   }
   switch (groups) {
     case 1: return pt::launch_pt<pt::Pt1>(in1, in2, out, B, C, H, W, Ho, Wo, off, layout, divisor, stream);

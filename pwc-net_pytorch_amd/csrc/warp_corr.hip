@@ -531,6 +531,10 @@ static bool make_prob(const void* f1, const void* x2, const void* flow, void* x2
       *T = 3;
     }
   }
+  // the instantiated (R, T) shapes: the per-level choices above (warp_corr_band's list)
+  const bool inst = (*R == 3 && *T == 1) || (*R == 2 && *T == (warp ? 3 : 1)) ||
+                    (*R == 3 && *T == 3 && warp);
+  if (!inst) return false;
   // a level whose all-channel staging exceeds the LDS runs as two launches (config-4 Sintel l1,
   // 128 channels x 32 columns: a lower band measured 2x slower than warp + row-band
   // correlation, profiles/r03e_band_fp16.txt)
@@ -581,27 +585,18 @@ hipError_t warp_corr_band(const void* f1, const void* x2, const void* flow, void
   size_t lds;
   if (!make_prob(f1, x2, flow, x2w, out, B, C, H, W, divisor, warp, &R, &T, &P, &lds))
     return hipErrorNotSupported;
-#define PWC_BAND32(RR, TT)                                                                   \
-  if (R == RR && T == TT && dtype == 0)                                                      \
-    return warp ? launch<float, RR, TT, true>(P, lds, stream)                                \
-                : launch<float, RR, TT, false>(P, lds, stream);
-#define PWC_BAND(RR, TT)                                                                     \
-  if (R == RR && T == TT && dtype == 1)                                                      \
-    return warp ? launch<__half, RR, TT, true>(P, lds, stream)                               \
-                : launch<__half, RR, TT, false>(P, lds, stream);                             \
-  PWC_BAND32(RR, TT)
-  // the per-level choices of make_prob (and its lower-band fallbacks) in both storage types;
-  // two more fp32 shapes the band tests force through the band_r / band_t knobs
-  PWC_BAND(3, 1)
-  PWC_BAND(2, 1)
-  PWC_BAND(1, 1)
-  PWC_BAND(2, 3)
-  PWC_BAND(3, 3)
-  PWC_BAND(1, 3)
-  PWC_BAND32(4, 3)
-  PWC_BAND32(6, 1)
+#define PWC_BAND(RR, TT, WW)                                                                 \
+  if (R == RR && T == TT && (warp != 0) == WW)                                               \
+    return dtype == 1 ? launch<__half, RR, TT, WW>(P, lds, stream)                           \
+                      : launch<float, RR, TT, WW>(P, lds, stream);
+  // the per-level choices of make_prob in both storage types: l0 (3, 1), l1 (2, 3) fused or
+  // (2, 1) plain, l2 and larger fused (3, 3)
+  PWC_BAND(3, 1, true)
+  PWC_BAND(3, 1, false)
+  PWC_BAND(2, 3, true)
+  PWC_BAND(2, 1, false)
+  PWC_BAND(3, 3, true)
 #undef PWC_BAND
-#undef PWC_BAND32
   return hipErrorNotSupported;
 }
 

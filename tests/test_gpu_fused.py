@@ -27,7 +27,7 @@ LEVELS = [(2, 192, 6, 7), (2, 128, 12, 14), (2, 96, 24, 28), (1, 64, 48, 56), (1
 RAGGED = [(1, 8, 5, 3), (2, 16, 7, 9), (1, 24, 13, 15), (1, 12, 2, 2), (1, 40, 11, 30),
           (3, 3, 9, 4)]
 # band configurations (R parity rows, T displacement rows per workgroup[, channel groups])
-CFGS = ["", "2,1", "3,3", "4,3", "6,1,1", "2,3,5"]
+CFGS = ["", "3,1", "2,3", "3,3", "3,1,1", "2,3,5"]
 
 
 def _t(a, dtype=torch.float32):

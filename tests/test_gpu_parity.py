@@ -443,6 +443,66 @@ def test_warp_fp16():
     np.testing.assert_allclose(_np(out), ref, rtol=2e-3, atol=5e-3)
 
 
+LOW = [(torch.float16, 2e-3), (torch.bfloat16, 1.6e-2)]
+
+
+@pytest.mark.parametrize("dtype,rtol", LOW, ids=["fp16", "bf16"])
+def test_low_precision_warp_upsample_backward_into(dtype, rtol):
+    """fp16 / bf16 storage through every op that takes it: warp (small and l4-sized images),
+    upsample+warp, Correlation backward (Corr9 and the s2 = 1 shape) and the activated strided
+    write of pwc_corr_forward_into -- against the oracle on the stored (rounded) inputs, fp32
+    arithmetic, tolerance one storage ulp relative to the output's magnitude."""
+    from pwcnet_amd.ops import (corr_backward, corr_forward, corr_forward_into,
+                                upsample_warp_forward, warp_forward)
+
+    def close(got, ref):
+        got = _np(got)
+        np.testing.assert_allclose(got, ref, rtol=rtol, atol=1e-4 + rtol * np.abs(ref).max())
+
+    rng = np.random.default_rng(61)
+    for shape in [(2, 16, 24, 28), (1, 16, 96, 112)]:
+        x = _t(_rand(rng, *shape), dtype)
+        f = _t(rng.standard_normal((shape[0], 2) + shape[2:]) * 3, dtype)
+        close(warp_forward(x, f), O.warp_forward(_np(x), _np(f)))
+    x2 = _t(_rand(rng, 2, 16, 24, 28), dtype)
+    fc = _t(rng.standard_normal((2, 2, 12, 14)) * 2, dtype)
+    out, fup = upsample_warp_forward(x2, fc)
+    close(fup, O.flow_upsample2(_np(fc)))
+    close(out, O.warp_forward(_np(x2), _np(fup)))
+    for B, C, H, W, pad, k, md, s1, s2 in [(2, 32, 24, 28, 9, 1, 9, 1, 2),
+                                           (1, 16, 17, 23, 4, 1, 4, 1, 1)]:
+        a, b = _t(_rand(rng, B, C, H, W), dtype), _t(_rand(rng, B, C, H, W), dtype)
+        OC, Ho, Wo = O.corr_output_shape(H, W, pad, k, md, s1, s2)
+        g = _t(_rand(rng, B, OC, Ho, Wo), dtype)
+        g1, g2 = corr_backward(a, b, g, pad, k, md, s1, s2)
+        assert g1.dtype == dtype and g2.dtype == dtype
+        r1, r2 = O.corr_backward(_np(a), _np(b), _np(g), pad, k, md, s1, s2)
+        close(g1, r1)
+        close(g2, r2)
+    a, b = _t(_rand(rng, 2, 16, 12, 14), dtype), _t(_rand(rng, 2, 16, 12, 14), dtype)
+    buf = torch.full((2, 16 + 83, 12, 14), -3.0, device=DEV, dtype=dtype)
+    corr_forward_into(a, b, buf[:, 16:97], 9, 1, 9, 1, 2, negative_slope=0.1)
+    ref = torch.nn.functional.leaky_relu(corr_forward(a, b, 9, 1, 9, 1, 2).float(), 0.1)
+    close(buf[:, 16:97], _np(ref))
+    assert bool((buf[:, :16] == -3.0).all()) and bool((buf[:, 97:] == -3.0).all())
+
+
+@pytest.mark.parametrize("case", [(1, 512, 6, 7), (2, 448, 5, 9)],
+                         ids=lambda s: "B{}C{}_{}x{}".format(*s))
+def test_corr_forward_wide_small_levels_channel_split(case):
+    """Small images with too many channels for the band kernel's LDS (and rows that are not
+    16-B aligned): the whole-parity-half kernel with channel slices into the workspace and its
+    fixed-order reduce (corr_small.hip) -- oracle parity and bitwise repeatability."""
+    from pwcnet_amd.ops import corr_forward
+    B, C, H, W = case
+    rng = np.random.default_rng(67)
+    a, b = _t(_rand(rng, B, C, H, W)), _t(_rand(rng, B, C, H, W))
+    out = corr_forward(a, b, 9, 1, 9, 1, 2)
+    np.testing.assert_allclose(_np(out), O.corr_forward(_np(a), _np(b), 9, 1, 9, 1, 2),
+                               rtol=1e-5, atol=1e-5)
+    assert torch.equal(out, corr_forward(a, b, 9, 1, 9, 1, 2))
+
+
 # ---------------------------------------------------------------------------------------
 # full BASELINE sizes: size-independent properties + full oracle compare (seconds on CPU)
 # ---------------------------------------------------------------------------------------

@@ -2,6 +2,7 @@
 # Round profile: bench JSON, per-level kernel times (kbench), rocprofv3 kernel-trace stats of
 # the same bench command, and the PMC passes (FETCH_SIZE / WRITE_SIZE, one counter per pass)
 # for the l4 correlation kernel.  Writes gpurun_out/prof_<tag>.
+# (Round 1 recipe: its PMC passes name corr_fwd_ring, the l4 kernel of rounds 1-2, removed in round 3.)
 set -o pipefail
 TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
