@@ -295,8 +295,8 @@ __global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__
 
 }  // namespace bwdrows
 
-// Measurement knobs (PWC_DEBUG / pwc_set_debug): bwd_rows=0 disables the kernel; bwd_r, bwd_ct
-// force a band height and channels per item; bwd_slices the channel slices.
+// Measurement knobs (PWC_DEBUG / pwc_set_debug): bwd_rows=0 disables the kernel; bwd_r forces a
+// band height, bwd_slices the channel slices.
 hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* gout, void* g1,
                                   void* g2, int B, int C, int H, int W, float divisor,
                                   hipStream_t stream) {
@@ -325,7 +325,6 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
     break;
   }
   R = debug_knob("bwd_r", R);
-  CT = debug_knob("bwd_ct", CT);
   g.R = R;
   g.I = 9 * R * 2 * g.S;
   if (R < 1 || g.I > NT) return hipErrorNotSupported;
@@ -382,14 +381,6 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   PWC_BWD(true, 8, 2)
   PWC_BWD(true, 8, 4)
   PWC_BWD(true, 8, 8)
-  PWC_BWD(true, 4, 2)
-  PWC_BWD(true, 4, 4)
-  PWC_BWD(true, 4, 8)
-  PWC_BWD(false, 8, 8)
-  PWC_BWD(false, 8, 16)
-  PWC_BWD(false, 8, 32)
-  PWC_BWD(false, 4, 8)
-  PWC_BWD(false, 4, 16)
   PWC_BWD(false, 2, 4)
   PWC_BWD(false, 2, 8)
 #undef PWC_BWD

@@ -59,7 +59,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int round64(int v) { return (v + 63) / 64 * 64; }
-constexpr int next_8mod16(int v) { return v + ((8 - v % 16) + 16) % 16; }
 
 // T: storage type (float or __half; arithmetic fp32); S2: displacement stride (2: rows of ONE
 // parity per workgroup; 1: consecutive rows); R: output rows per workgroup; TWP: column tile
@@ -68,17 +67,16 @@ constexpr int next_8mod16(int v) { return v + ((8 - v % 16) + 16) % 16; }
 // P2 (fp16 storage only): LDS holds channel PAIRS -- pixel x of channels (c, c+1) as one
 // half2 dword, interleaved by the loader on the way in -- and every product pair is one
 // v_dot2_f32_f16 (two fp16 products, fp32 accumulation): per channel pair the fp32 kernel's LDS
-// traffic and instruction count, i.e. half of them per channel against v_fma_mix.
+// traffic and instruction count.  fp16 storage always takes the pair layout.
 template <typename T, int S2_, int R_, int TWP_, int CC_, int NS_, bool P2_ = false>
 struct Geo {
   using Elem = T;
   static constexpr int S2 = S2_, R = R_, TWP = TWP_, CC = CC_, NS = NS_;
   static constexpr bool H16 = sizeof(T) == 2;            // fp16 storage (and output)
   static constexpr bool P2 = P2_;
-  static_assert(!P2 || H16, "channel pairs are an fp16-storage layout");
-  static constexpr bool L16 = H16 && !P2;                // LDS holds single halves
+  static_assert(P2 == H16, "fp16 storage is staged as channel pairs (and only fp16)");
   static constexpr int CPU = P2 ? 2 : 1;                 // channels per ring unit
-  static constexpr int EPQ = L16 ? 8 : 4;                // LDS elements (pixels) per quad
+  static constexpr int EPQ = 4;                          // LDS elements (dwords) per quad
   static constexpr int OEPQ = 16 / (int)sizeof(T);       // output pixels per 16-B quad
   static constexpr int NPY = S2 == 2 ? 2 : 1;            // row parities split over workgroups
   static constexpr int TWQ = TWP / EPQ;                  // tile quads per row (LDS)
@@ -91,10 +89,10 @@ struct Geo {
   static constexpr int BS = H16 ? 8 : (NSEG + NB - 1) / NB;
   // LDS row stride in quads: a ds_read_b128 lane group holds 8 segments of unit A and 8 of a
   // unit whose row differs by one, so their 16-B slots (mod 256 B) are disjoint iff S is odd
-  // (fp32 / pairs: 2 quads per segment) or S = 8 mod 16 (halves: 1 quad per segment)
-  static constexpr int S = L16 ? next_8mod16(TWQ + 2 * HQ) : ((TWQ + 2 * HQ) | 1);
-  static constexpr int NWQ = L16 ? 3 : (S2 == 2 ? 6 : 4);  // window quads read per unit
-  static constexpr int NFQ = L16 ? 1 : 2;                // f1 quads read per unit
+  // (2 quads per segment)
+  static constexpr int S = (TWQ + 2 * HQ) | 1;
+  static constexpr int NWQ = S2 == 2 ? 6 : 4;            // window quads read per unit
+  static constexpr int NFQ = 2;                          // f1 quads read per unit
   static constexpr int F2R = R + 8;                      // f2 rows (tj = -4..4)
   static constexpr int F2Q = round64(F2R * S);           // quads of the f2 part of a channel
   static constexpr int F1Q = round64(R * S);
@@ -121,7 +119,7 @@ struct Geo {
   static constexpr int WAITN = (NS - 3) * CC * IPC < 63 ? (NS - 3) * CC * IPC : 63;
   static_assert(S2 == 1 || S2 == 2, "displacement stride");
   static_assert(TWP % 8 == 0 && TWP % EPQ == 0 && BS <= 8, "8-pixel segments, <= 8 per block");
-  static_assert(L16 ? S % 16 == 8 : S % 2 == 1, "conflict-free row stride");
+  static_assert(S % 2 == 1, "conflict-free row stride");
   static_assert(NS >= 4, "ring depth");
   static_assert(THREADS <= 1024 && LDS_BYTES <= 160 * 1024, "workgroup resources");
   static_assert(CH_B <= 32768, "a channel fits one 32 KiB window");
@@ -220,26 +218,6 @@ __device__ __forceinline__ void fma_ti(float (&acc)[9][8], const f32x4 (&w)[6],
   }
 }
 
-// fp16 storage: the same products from half operands with fp32 accumulation (fma of two
-// widened halves -> v_fma_mix_f32); window element 0 sits at element WEL of quad 0.
-template <int S2, int WEL, int T0, int T1>
-__device__ __forceinline__ void fma_ti_h(float (&acc)[9][8], const f32x4 (&w)[6],
-                                         const f32x4 (&f)[2]) {
-  const f16x8 a = __builtin_bit_cast(f16x8, f[0]);
-  const f16x8 w0 = __builtin_bit_cast(f16x8, w[0]);
-  const f16x8 w1 = __builtin_bit_cast(f16x8, w[1]);
-  const f16x8 w2 = __builtin_bit_cast(f16x8, w[2]);
-#pragma unroll
-  for (int ti = T0; ti < T1; ++ti) {
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int j = WEL + p + S2 * ti;  // 0..23
-      const _Float16 wv = j < 8 ? w0[j] : j < 16 ? w1[j - 8] : w2[j - 16];
-      acc[ti][p] = fmaf((float)a[p], (float)wv, acc[ti][p]);
-    }
-  }
-}
-
 // Channel pairs: acc[ti][p] += f1[c][p] * w[c][p + S2 ti] + f1[c+1][p] * w[c+1][p + S2 ti]
 // as one v_dot2_f32_f16 per (ti, p); every LDS dword is one pixel's (c, c+1) half2.
 typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
@@ -315,14 +293,7 @@ __device__ __forceinline__ void channel_body(uint32_t w_, uint32_t f_, float (&a
                                              const f32x4 (&wc)[6], const f32x4 (&fc)[2],
                                              f32x4 (&wn)[6], f32x4 (&fn)[2]) {
   constexpr bool RD = !(M & 1), FM = !(M & 2);
-  if constexpr (G::L16) {
-    constexpr int WEL = G::S2 == 2 ? 0 : 4;
-    if constexpr (RD) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
-    if constexpr (FM) fma_ti_h<G::S2, WEL, 0, 5>(acc, wc, fc);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (RD) read2<IMM + 32, IMM>(w_, f_, wn[2], fn[0]);
-    if constexpr (FM) fma_ti_h<G::S2, WEL, 5, 9>(acc, wc, fc);
-  } else if constexpr (G::S2 == 2) {
+  if constexpr (G::S2 == 2) {
     if constexpr (RD) read2<IMM, IMM + 16>(w_, w_, wn[0], wn[1]);
     if constexpr (FM) fma_unit<G, 0, 2>(acc, wc, fc);
     __builtin_amdgcn_sched_barrier(0);
@@ -572,9 +543,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
     const bool active = gi < G::NG && sp < G::BS && seg < G::NSEG && (p < 8 || hasb);
     const int sg = seg < G::NSEG ? seg : 0;  // a duplicate address for idle lanes (broadcast)
     // window: from pixel x0 - 4 S2, i.e. padded pixel 8 seg + 8 - 4 S2 (fp32: quad 2 seg or
-    // 2 seg + 1; fp16: quad seg, element 0 or 4); f1: padded pixel 8 seg + 8
-    const int wq = G::L16 ? sg : 2 * sg + (G::S2 == 2 ? 0 : 1);
-    const int fq = G::L16 ? sg + 1 : 2 * sg + 2;
+    // 2 seg + 1); f1: padded pixel 8 seg + 8
+    const int wq = 2 * sg + (G::S2 == 2 ? 0 : 1);
+    const int fq = 2 * sg + 2;
     uint32_t wa[G::NBASE], fa[G::NBASE];
 #pragma unroll
     for (int k = 0; k < G::NBASE; ++k) {
@@ -594,15 +565,10 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
       acc[0][0] = (float)C;
     } else {
       __builtin_amdgcn_s_barrier();  // B_0: stage 0 landed
-      if constexpr (G::L16) {
-        read2<0, 16>(wa[0], wa[0], wA[0], wA[1]);
-        read2<32, 0>(wa[0], fa[0], wA[2], fA[0]);
-      } else {
-        read2<0, 16>(wa[0], wa[0], wA[0], wA[1]);
-        read2<32, 48>(wa[0], wa[0], wA[2], wA[3]);
-        if constexpr (G::S2 == 2) read2<64, 80>(wa[0], wa[0], wA[4], wA[5]);
-        read2<0, 16>(fa[0], fa[0], fA[0], fA[1]);
-      }
+      read2<0, 16>(wa[0], wa[0], wA[0], wA[1]);
+      read2<32, 48>(wa[0], wa[0], wA[2], wA[3]);
+      if constexpr (G::S2 == 2) read2<64, 80>(wa[0], wa[0], wA[4], wA[5]);
+      read2<0, 16>(fa[0], fa[0], fA[0], fA[1]);
       switch (abl >> 3) {
         case 0: compute_loop<G, 0>(CU, nst, wa, fa, acc, wA, fA, wB, fB); break;
         case 1: compute_loop<G, 1>(CU, nst, wa, fa, acc, wA, fA, wB, fB); break;
@@ -750,29 +716,27 @@ static hipError_t pick(const void* in1, const void* in2, void* out, int B, int C
   // 17.2 us against 2 x 8; Corr4, Sintel fp32/fp16 l3/l4; profiles/r02d_stream_ring_sweep.txt),
   // where one launch's store tail overlaps the next one's loop; inside the bench step, where
   // it cannot, all three rings measure the same 19.1-19.4 us (profiles/r02d_bench_ring_ab.txt)
-  // fp16: channel pairs through v_dot2_f32_f16 (stream_p2=0: single halves, v_fma_mix)
+  // fp16: channel pairs through v_dot2_f32_f16 (corr_stream_accepts guarantees C % 16 == 0)
   if constexpr (sizeof(T) == 2) {
-    if (debug_knob("stream_p2", 1) && C % 16 == 0) {
-      // 4-row bands when 3-row bands give few workgroups (about one round): config-4 Sintel
-      // l3 (B=16, 64 x 56 x 128) 41.6 -> 28.0 us; l4 (1216 workgroups) stays at 3 (63.3 against
-      // 66.4 us; 2 rows 75.4); profiles/r02e_stream_fp16_rows.txt
-      const int hp = S2 == 2 ? (H + 1) / 2 : H;
-      const long long nblk3 = (long long)B * (S2 == 2 ? 2 : 1) * ((hp + 2) / 3) *
-                              ((W + TWP - 1) / TWP);
-      if (debug_knob("stream_r", nblk3 <= 384 ? 4 : 3) == 4)
-        return launch<Geo<T, S2, 4, TWP, 2, 4, true>>(in1, in2, out, B, C, H, W, layout, divisor,
-                                                      stream);
-      return launch<Geo<T, S2, 3, TWP, 2, 4, true>>(in1, in2, out, B, C, H, W, layout, divisor,
+    // 4-row bands when 3-row bands give few workgroups (about one round): config-4 Sintel
+    // l3 (B=16, 64 x 56 x 128) 41.6 -> 28.0 us; l4 (1216 workgroups) stays at 3 (63.3 against
+    // 66.4 us; 2 rows 75.4); profiles/r02e_stream_fp16_rows.txt
+    const int hp = S2 == 2 ? (H + 1) / 2 : H;
+    const long long nblk3 = (long long)B * (S2 == 2 ? 2 : 1) * ((hp + 2) / 3) *
+                            ((W + TWP - 1) / TWP);
+    if (debug_knob("stream_r", nblk3 <= 384 ? 4 : 3) == 4)
+      return launch<Geo<T, S2, 4, TWP, 2, 4, true>>(in1, in2, out, B, C, H, W, layout, divisor,
                                                     stream);
-    }
-  }
-  // stride-1 displacements (Corr4, CostVolumeLayer): the 4 x 4 ring needs more than the 256
-  // VGPRs (~640 spilled to scratch), 2 x 4 none, at the same time (l4 16.9-17.0 us against
-  // 16.9-17.3 over 300 launches each; profiles/r02e_corr4_ring.txt)
-  if constexpr (S2 == 1)
+    return launch<Geo<T, S2, 3, TWP, 2, 4, true>>(in1, in2, out, B, C, H, W, layout, divisor,
+                                                  stream);
+  } else if constexpr (S2 == 1) {
+    // stride-1 displacements (Corr4, CostVolumeLayer): the 4 x 4 ring needs more than the 256
+    // VGPRs (~640 spilled to scratch), 2 x 4 none, at the same time (l4 16.9-17.0 us against
+    // 16.9-17.3 over 300 launches each; profiles/r02e_corr4_ring.txt)
     return launch<Geo<T, S2, 3, TWP, 2, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
-  else
+  } else {
     return launch<Geo<T, S2, 3, TWP, 4, 4>>(in1, in2, out, B, C, H, W, layout, divisor, stream);
+  }
 }
 
 }  // namespace stream

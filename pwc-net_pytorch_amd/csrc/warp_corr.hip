@@ -589,14 +589,17 @@ hipError_t warp_corr_band(const void* f1, const void* x2, const void* flow, void
   if (R == RR && T == TT && (warp != 0) == WW)                                               \
     return dtype == 1 ? launch<__half, RR, TT, WW>(P, lds, stream)                           \
                       : launch<float, RR, TT, WW>(P, lds, stream);
-  // the per-level choices of make_prob in both storage types: l0 (3, 1), l1 (2, 3) fused or
-  // (2, 1) plain, l2 and larger fused (3, 3)
+#define PWC_BAND32(RR, TT)                                                                   \
+  if (R == RR && T == TT && !warp && dtype == 0) return launch<float, RR, TT, false>(P, lds, stream);
+  // the per-level choices of make_prob: l0 (3, 1), l1 (2, 3) and l2 and larger (3, 3) fused in
+  // both storage types; the plain correlation (corr_forward_path: fp32 l0 / l1) (3, 1), (2, 1)
   PWC_BAND(3, 1, true)
-  PWC_BAND(3, 1, false)
   PWC_BAND(2, 3, true)
-  PWC_BAND(2, 1, false)
   PWC_BAND(3, 3, true)
+  PWC_BAND32(3, 1)
+  PWC_BAND32(2, 1)
 #undef PWC_BAND
+#undef PWC_BAND32
   return hipErrorNotSupported;
 }
 
