@@ -50,10 +50,27 @@ struct Geo {
   int cps;   // channels per slice (grid.y), a multiple of ck
   int lw;    // load items per staged row: W / 4 (VEC) or W
   int g2v;   // VEC: gradient 2's gO values from aligned quads (else dword loads)
+  int census;  // measurement only (knob bwd_census): phase stamps -> g_bwd_census
   float inv_lw, inv_NR, inv_I, inv_S, inv_R;
 };
 
 __device__ __forceinline__ int qdiv(int x, float inv) { return (int)(((float)x + 0.5f) * inv); }
+
+// Phase census (measurement only, knob bwd_census): s_memrealtime (100 MHz) of thread 0 of
+// workgroup b -> g_bwd_census[b * 8 + k], a branch-free buffer store (off unless g.census)
+typedef unsigned int u32x2b __attribute__((ext_vector_type(2)));
+__device__ unsigned long long g_bwd_census[4096 * 8];
+#define BWD_MARK(k)                                                                          \
+  do {                                                                                       \
+    const unsigned lin_ = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;    \
+    const bool on_ = g.census && threadIdx.x == 0 && lin_ < 4096;                            \
+    const unsigned long long ts_ = __builtin_amdgcn_s_memrealtime();                         \
+    __builtin_amdgcn_raw_buffer_store_b64(                                                   \
+        __builtin_bit_cast(u32x2b, ts_),                                                     \
+        __builtin_amdgcn_make_buffer_rsrc((void*)g_bwd_census, (short)0,                     \
+                                          (int)sizeof(g_bwd_census), 0x00020000),            \
+        on_ ? (int)((lin_ * 8 + (k)) * 8) : (int)0x80000000, 0, 0);                          \
+  } while (0)
 
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -78,6 +95,7 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
   float* stg = lds;
   f32x4* part = reinterpret_cast<f32x4*>(lds + g.stf);
   const int t = threadIdx.x;
+  BWD_MARK(0);
   const int R = g.R, NR = R + 8;
   const int unit = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring bands share an L2
   const int b = unit % g.nb, np = unit / g.nb;
@@ -204,6 +222,7 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
     }
     if (cb + g.ck < ce) issue(cb + g.ck);
     lds_barrier();
+    BWD_MARK(cb == cs ? 1 : 3);  // chunk staged (1: the first -- gO registers landed too)
     if (active) {
 #pragma unroll
       for (int j = 0; j < CT; ++j) {
@@ -226,6 +245,7 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
       }
     }
     lds_barrier();
+    BWD_MARK(cb == cs ? 2 : 4);  // chunk computed
     // ---- epilogue: the 9 tj partials of each (channel, pixel) summed in tj order ----
     if (VEC) {
       const int Q = W >> 2;
@@ -274,6 +294,7 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
       }
     }
   }
+  BWD_MARK(5);  // stores issued
 }
 
 // Both gradients in ONE launch: grid.z = 0 computes g1 from f2, grid.z = 1 g2 from f1 (the
@@ -341,6 +362,7 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   }
   g.lw = vec ? W / 4 : W;
   g.g2v = debug_knob("bwd_g2v", 1);
+  g.census = debug_knob("bwd_census", 0);
   g.nld = g.ck * (R + 8) * g.lw;
   // channel slices (grid.y) up to one workgroup per CU over both gradients (grid.z): the
   // slices of a band are independent (every gradient element is one channel's) but each
@@ -385,6 +407,17 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   PWC_BWD(false, 2, 8)
 #undef PWC_BWD
   return hipErrorNotSupported;
+}
+
+// measurement only: copy (dst) or clear (dst == null) the phase stamps of bwd_census launches
+extern "C" __attribute__((visibility("default"))) int pwc_debug_bwd_census(void* dst, int n) {
+  if (dst == nullptr) {
+    static unsigned long long zeros[4096 * 8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(bwdrows::g_bwd_census), zeros, sizeof(zeros)) ==
+           hipSuccess;
+  }
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(bwdrows::g_bwd_census),
+                             sizeof(unsigned long long) * (size_t)n) == hipSuccess;
 }
 
 }  // namespace pwc
