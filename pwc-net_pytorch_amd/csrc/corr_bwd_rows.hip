@@ -56,10 +56,12 @@ struct Geo {
 
 __device__ __forceinline__ int qdiv(int x, float inv) { return (int)(((float)x + 0.5f) * inv); }
 
-// Phase census (measurement only, knob bwd_census): s_memrealtime (100 MHz) of thread 0 of
-// workgroup b -> g_bwd_census[b * 8 + k], a branch-free buffer store (off unless g.census)
+// Phase census (measurement only: a `make CENSUS=1` build + knob bwd_census): s_memrealtime
+// (100 MHz) of thread 0 of workgroup b -> g_bwd_census[b * 8 + k], a branch-free buffer store.
+// The product build compiles the marks out (each store would add to the waits on vmcnt).
 typedef unsigned int u32x2b __attribute__((ext_vector_type(2)));
 __device__ unsigned long long g_bwd_census[4096 * 8];
+#ifdef PWC_CENSUS
 #define BWD_MARK(k)                                                                          \
   do {                                                                                       \
     const unsigned lin_ = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;    \
@@ -71,6 +73,11 @@ __device__ unsigned long long g_bwd_census[4096 * 8];
                                           (int)sizeof(g_bwd_census), 0x00020000),            \
         on_ ? (int)((lin_ * 8 + (k)) * 8) : (int)0x80000000, 0, 0);                          \
   } while (0)
+#else
+#define BWD_MARK(k) \
+  do {            \
+  } while (0)
+#endif
 
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");

@@ -5,7 +5,7 @@ workgroup's own entry (the XCDs' clocks differ by ~2 us) and, for the entry itse
 the earliest entry of the same XCD (blockIdx % 8).  Workgroups are split into dispatch rounds
 by entry time.
 
-    python tools/bwd_phases.py --level 4 [--knobs bwd_pipe=1]
+    make -C pwc-net_pytorch_amd/csrc -B CENSUS=1 && python tools/bwd_phases.py --level 4
 """
 import argparse
 import ctypes
@@ -55,6 +55,8 @@ def main():
     _lib.set_debug("")
     t = buf.reshape(4096, 8).astype(np.int64)
     ids = np.nonzero(t[:, 0] > 0)[0]
+    if len(ids) == 0:
+        sys.exit("no census stamps: build the library with `make CENSUS=1` first")
     t = t[ids]
     xcd = ids % 8
     entry = np.zeros(len(t))
