@@ -49,7 +49,6 @@ struct Geo {
   int nld;   // staging load items per chunk: ck * (R + 8) * (W / 4 if VEC else W)
   int cps;   // channels per slice (grid.y), a multiple of ck
   int lw;    // load items per staged row: W / 4 (VEC) or W
-  int g2v;   // VEC: gradient 2's gO values from aligned quads (else dword loads)
   int census;  // measurement only (knob bwd_census): phase stamps -> g_bwd_census
   float inv_lw, inv_NR, inv_I, inv_S, inv_R;
 };
@@ -141,6 +140,11 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
   }
 
   // ---- compute item (tj, band row r, column parity q, segment s) ----
+  // Measured and not kept (r03h): items over three tj rows (the 3 tj summed in registers: a
+  // third of the partial stores and epilogue reads, 108 gO registers, l4 as ONE round of
+  // 6-row bands in 512-thread workgroups): l4 40.4 us against 36.7 -- its start-up 21 us
+  // against 5.9 per round (both gradients' gO, 56 MB, loaded at once) -- and l3 27.8 against
+  // 21.8 (profiles/r03h_corr_bwd_tg.txt)
   const int grp = qdiv(t, g.inv_I), it = t - grp * g.I;
   const bool active = grp < g.G;
   const int s = it - qdiv(it, g.inv_S) * g.S;
@@ -149,8 +153,13 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
   rest >>= 1;
   const int r = rest - qdiv(rest, g.inv_R) * R, tj = qdiv(rest, g.inv_R);
   const int whq = (W - q + 1) >> 1;  // columns of this parity
-  // the 36 gO values of this item, zero where the forward output does not exist
+  // the 36 gO values of this item, zero where the forward output does not exist.  Every load
+  // is issued before the first use (straight-line code, one wait): loads and uses interleaved
+  // per displacement made the compiler wait for each displacement's loads in turn (9
+  // dependent memory round trips per workgroup start).
   float gv[D][4];
+  constexpr int NQ = GRAD == 1 ? 2 : 3;  // quads per displacement (VEC)
+  f32x4 raw[VEC ? D : 1][NQ];
   {
     const int Y = GRAD == 1 ? r0 + r : r0 + r - tj + 4;  // gO parity row
     const bool rok = active && Y >= 0 && Y < hp && r0 + r < hp;
@@ -158,28 +167,17 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
     for (int ti = 0; ti < D; ++ti) {
       const int X0 = GRAD == 1 ? 4 * s : 4 * s - ti + 4;  // gO parity column of kk = 0
       const uint32_t rowoff = (uint32_t)(tj * D + ti) * plane + (uint32_t)(2 * Y + p) * W;
-      if (VEC && GRAD == 1) {
+      if constexpr (VEC && GRAD == 1) {
         const uint32_t o = rok ? (rowoff + 8 * s) * 4u : kOOB;
-        const f32x4 a = ld4(rsg, o), c4 = ld4(rsg, o + 16u);
-        gv[ti][0] = q ? a.y : a.x;
-        gv[ti][1] = q ? a.w : a.z;
-        gv[ti][2] = q ? c4.y : c4.x;
-        gv[ti][3] = q ? c4.w : c4.z;
-      } else if (VEC && g.g2v) {
+        raw[ti][0] = ld4(rsg, o);
+        raw[ti][1] = ld4(rsg, o + 16u);
+      } else if constexpr (VEC) {
         // raster columns 2*X0 + q + 2kk (kk = 0..3) from three aligned quads [b, b + 12);
         // b = 2*X0 - 2*(ti & 1).  X0 < 0 only for ti >= 5, so rowoff + b stays >= 0 (the
         // quads then start in the previous plane's data, masked below)
-        const int sh = 2 * (ti & 1);
-        const uint32_t o = rok ? (rowoff + 2 * X0 - sh) * 4u : kOOB;
-        const f32x4 a = ld4(rsg, o), bq = ld4(rsg, o + 16u), c4 = ld4(rsg, o + 32u);
-        const float w12[12] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c4.x, c4.y, c4.z, c4.w};
+        const uint32_t o = rok ? (rowoff + 2 * X0 - 2 * (ti & 1)) * 4u : kOOB;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int X = X0 + kk;
-          const bool ok = X >= 0 && X < whq;
-          const float v = q ? w12[sh + 2 * kk + 1] : w12[sh + 2 * kk];
-          gv[ti][kk] = ok ? v : 0.f;
-        }
+        for (int k = 0; k < NQ; ++k) raw[ti][k] = ld4(rsg, o + 16u * k);
       } else {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
@@ -190,6 +188,35 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
       }
     }
   }
+  if constexpr (VEC) {
+#pragma unroll
+    for (int ti = 0; ti < D; ++ti) {
+      if constexpr (GRAD == 1) {
+        const f32x4 a = raw[ti][0], c4 = raw[ti][1];
+        gv[ti][0] = q ? a.y : a.x;
+        gv[ti][1] = q ? a.w : a.z;
+        gv[ti][2] = q ? c4.y : c4.x;
+        gv[ti][3] = q ? c4.w : c4.z;
+      } else {
+        const int X0 = 4 * s - ti + 4, sh = 2 * (ti & 1);
+        const f32x4 a = raw[ti][0], bq = raw[ti][1], c4 = raw[ti][2];
+        const float w12[12] = {a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int X = X0 + kk;
+          const bool ok = X >= 0 && X < whq;
+          const float v = q ? w12[sh + 2 * kk + 1] : w12[sh + 2 * kk];
+          gv[ti][kk] = ok ? v : 0.f;
+        }
+      }
+    }
+  }
+  // every gO value has landed before the chunk loop: left pending, the waits the compiler
+  // places for them inside the loop also wait for the next chunk's staging loads
+#pragma unroll
+  for (int ti = 0; ti < D; ++ti)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) asm volatile("" : "+v"(gv[ti][kk]));
   const int krow = GRAD == 1 ? r + tj : r - tj + 8;  // staged feature row
   const int wbase = (krow * 2 + q) * g.Wf + 4 * s;
   const int cstride = NR * 2 * g.Wf;
@@ -231,24 +258,33 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
     lds_barrier();
     BWD_MARK(cb == cs ? 1 : 3);  // chunk staged (1: the first -- gO registers landed too)
     if (active) {
+      // channel j of the chunk: 3 window quads, 36 FMAs.  The next channel's quads are read
+      // before this channel's FMAs (double-buffered; the partial store between channels would
+      // otherwise pin each channel's reads behind the previous store).  No `c < cn` guard: a
+      // short chunk's missing channels are staged as zeros and their partials never summed.
+      auto rd = [&](int j, f32x4(&b)[3]) {
+        const float* pw = stg + (grp + j * g.G) * cstride + wbase;
+        b[0] = *reinterpret_cast<const f32x4*>(pw);
+        b[1] = *reinterpret_cast<const f32x4*>(pw + 4);
+        b[2] = *reinterpret_cast<const f32x4*>(pw + 8);
+      };
+      f32x4 bA[3], bB[3];
+      rd(0, bA);
 #pragma unroll
       for (int j = 0; j < CT; ++j) {
-        const int c = grp + j * g.G;  // channel within the chunk (< ck)
+        f32x4(&cur)[3] = (j & 1) ? bB : bA;
+        f32x4(&nxt)[3] = (j & 1) ? bA : bB;
+        if (j + 1 < CT) rd(j + 1, nxt);
+        __builtin_amdgcn_sched_barrier(0);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        if (c < cn) {
-          const float* pw = stg + c * cstride + wbase;
-          const f32x4 q0 = *reinterpret_cast<const f32x4*>(pw);
-          const f32x4 q1 = *reinterpret_cast<const f32x4*>(pw + 4);
-          const f32x4 q2 = *reinterpret_cast<const f32x4*>(pw + 8);
-          const float w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y,
-                               q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+        const float w[12] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y,
+                             cur[1].z, cur[1].w, cur[2].x, cur[2].y, cur[2].z, cur[2].w};
 #pragma unroll
-          for (int ti = 0; ti < D; ++ti)
+        for (int ti = 0; ti < D; ++ti)
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-              acc[kk] = fmaf(gv[ti][kk], w[GRAD == 1 ? kk + ti : kk + 8 - ti], acc[kk]);
-        }
-        part[c * (D * RS2) + pbase] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+          for (int kk = 0; kk < 4; ++kk)
+            acc[kk] = fmaf(gv[ti][kk], w[GRAD == 1 ? kk + ti : kk + 8 - ti], acc[kk]);
+        part[(grp + j * g.G) * (D * RS2) + pbase] = f32x4{acc[0], acc[1], acc[2], acc[3]};
       }
     }
     lds_barrier();
@@ -306,7 +342,9 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
 
 // Both gradients in ONE launch: grid.z = 0 computes g1 from f2, grid.z = 1 g2 from f1 (the
 // two are independent; at the coarse levels each alone fills a fraction of the chip, so one
-// launch runs them side by side and saves a launch gap).
+// launch runs them side by side and saves a launch gap).  Measured and not kept (r03h): the two
+// gradients and channel slices of a band adjacent on one XCD, so that both read the band's gO
+// from one L2 in the same round (l4 36.7 -> 38.9 us).
 template <bool VEC, int CT, int ML, int NT>
 __global__ __launch_bounds__(NT, 1) void corr_bwd_rows(const float* __restrict__ f1,
                                                        const float* __restrict__ f2,
@@ -336,7 +374,6 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   const bool vec = W % 4 == 0 && (uintptr_t)in1 % 16 == 0 && (uintptr_t)in2 % 16 == 0 &&
                    (uintptr_t)gout % 16 == 0 && (uintptr_t)g1 % 16 == 0 &&
                    (uintptr_t)g2 % 16 == 0;
-  constexpr int NT = 768;
   const int hp = (H + 1) / 2;
   Geo g;
   g.Wq4 = (((W + 1) / 2) + 3) & ~3;
@@ -346,6 +383,7 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   // CT (channels per item and chunk) 8 on the 16-B path; 2 on the dword path (l0 / l1: more,
   // shorter chunks give more slices -- 10.6 -> 9.4 us at l0, 12.0 -> 11.6 at l1;
   // profiles/r02e_corr_bwd_slices.txt)
+  constexpr int NT = 768;
   int R = 1, CT = vec ? 8 : 2;
   for (int r : {3, 2, 1}) {
     if (9 * r * 2 * g.S > NT) continue;
@@ -368,7 +406,6 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
     if (g.G == 1) return hipErrorNotSupported;
   }
   g.lw = vec ? W / 4 : W;
-  g.g2v = debug_knob("bwd_g2v", 1);
   g.census = debug_knob("bwd_census", 0);
   g.nld = g.ck * (R + 8) * g.lw;
   // channel slices (grid.y) up to one workgroup per CU over both gradients (grid.z): the
