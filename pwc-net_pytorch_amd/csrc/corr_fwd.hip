@@ -541,7 +541,7 @@ int corr_forward_path(const void* in1, const void* in2, const void* out, int B, 
   return kPathOther;
 }
 
-// corr_rows.hip (row bands over full rows) serves l3-sized grids (it decides; PWC_ROWS).
+// corr_rows.hip (row bands over full rows) serves l2/l3-sized grids (it decides; PWC_DEBUG knob `rows`).
 
 // `workspace` (>= corr_workspace_bytes) enables channel splitting for grids too small to fill
 // the chip; null keeps one workgroup per tile over all channels.
