@@ -111,10 +111,6 @@ struct Geo {
   static constexpr int UPR = (TWP + 16) / 8;             // units per staged row
   static constexpr int NU = (F2R + R) * UPR;             // units per channel pair
   static constexpr int NIT = (NU + 63) / 64;             // loader iterations per pair
-  // P2 loader keeps two stages of register loads in flight when the workgroup runs at two
-  // waves per SIMD anyway (<= 8 waves: the second stage's registers fit under the compute
-  // waves' allocation); the 10-wave R = 4 form (three per SIMD, <= 168 VGPRs) keeps one
-  static constexpr bool LDB = P2 && NWC + 1 <= 8;
   static constexpr int OUT_B = 81 * R * PRQ * 16;
   static constexpr int LDS_BYTES = RING_B > OUT_B ? RING_B : OUT_B;
   static constexpr int NBASE = (RING_B + 32767) / 32768;  // 32 KiB address windows
@@ -425,30 +421,24 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
         __builtin_amdgcn_make_buffer_rsrc((void*)img1, (short)0, (int)img_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs2 =
         __builtin_amdgcn_make_buffer_rsrc((void*)img2, (short)0, (int)img_bytes, 0x00020000);
-    // one stage of register staging; a stage past the last is issued with an out-of-range
-    // offset (the buffer unit returns zeros without a memory access) so that the double-
-    // buffered schedule below is straight-line code
-    struct Buf {
-      f32x4 a2[G::CC][NI2], b2[G::CC][NI2], a1[G::CC][NI1], b1[G::CC][NI1];
-    };
-    auto issue = [&](Buf& x, int gs) {
+    f32x4 a2[G::CC][NI2], b2[G::CC][NI2], a1[G::CC][NI1], b1[G::CC][NI1];
+    auto issue = [&](int gs) {
 #pragma unroll
       for (int j = 0; j < G::CC; ++j) {
-        const int so =
-            gs < nst ? (int)((uint32_t)(2 * (gs * G::CC + j)) * plane_b) : (int)img_bytes;
+        const int so = (int)((uint32_t)(2 * (gs * G::CC + j)) * plane_b);
 #pragma unroll
         for (int it = 0; it < NI2; ++it) {
-          x.a2[j][it] = __builtin_bit_cast(
+          a2[j][it] = __builtin_bit_cast(
               f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs2, (int)rel2[it], so, 0));
-          x.b2[j][it] = __builtin_bit_cast(
+          b2[j][it] = __builtin_bit_cast(
               f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs2, (int)rel2[it],
                                                            so + (int)plane_b, 0));
         }
 #pragma unroll
         for (int it = 0; it < NI1; ++it) {
-          x.a1[j][it] = __builtin_bit_cast(
+          a1[j][it] = __builtin_bit_cast(
               f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs1, (int)rel1[it], so, 0));
-          x.b1[j][it] = __builtin_bit_cast(
+          b1[j][it] = __builtin_bit_cast(
               f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs1, (int)rel1[it],
                                                            so + (int)plane_b, 0));
         }
@@ -472,55 +462,30 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_stream(
       *reinterpret_cast<u32x4*>(base + 4 * dq) = q0;
       *reinterpret_cast<u32x4*>(base + 4 * dq + 4) = q1;
     };
-    auto write = [&](const Buf& x, int gs) {
+    auto write = [&](int gs) {
       float* slot = lds + (size_t)(gs % G::NS) * (G::SLOT_B / 4);
 #pragma unroll
       for (int j = 0; j < G::CC; ++j) {
         float* base = slot + j * (G::CH_B / 4);
 #pragma unroll
-        for (int it = 0; it < NI2; ++it) put(base, dq2[it], x.a2[j][it], x.b2[j][it]);
+        for (int it = 0; it < NI2; ++it) put(base, dq2[it], a2[j][it], b2[j][it]);
 #pragma unroll
-        for (int it = 0; it < NI1; ++it) put(base, dq1[it], x.a1[j][it], x.b1[j][it]);
+        for (int it = 0; it < NI1; ++it) put(base, dq1[it], a1[j][it], b1[j][it]);
       }
     };
-    auto bar = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
     if (abl & 2) {  // measurement: no staging (barriers only)
       for (int k = 0; k <= nst; ++k) __builtin_amdgcn_s_barrier();
-    } else if (G::LDB && (abl & 64)) {
-      // two stages of loads in flight: stage s is consumed (written to the ring) while stage
-      // s + 1's loads are still out, then its registers take stage s + 2's.  NS = 4: stages 0
-      // and 1 before B_0, stage s (>= 2) between B_{s-2} and B_{s-1}; nst is a multiple of 4.
-      static_assert(!G::LDB || G::NS == 4, "the schedule below is NS = 4's");
-      Buf A, Bq;
-      issue(A, 0);
-      issue(Bq, 1);
-      write(A, 0);
-      issue(A, 2);
-      write(Bq, 1);
-      issue(Bq, 3);
-      bar();  // B_0
-      for (int st = 2; st < nst; st += 2) {
-        write(A, st);
-        issue(A, st + 2);
-        bar();  // B_{st-1}
-        write(Bq, st + 1);
-        issue(Bq, st + 3);
-        bar();  // B_st
-      }
-      bar();  // B_{nst-1}
-      bar();  // B_nst
     } else {
-      Buf A;
-      if (nst > 0) issue(A, 0);
+      if (nst > 0) issue(0);
       int nw = 0;  // next stage to write
       for (int k = 0; k <= nst; ++k) {
         const int upto = min(k + G::NS - 3, nst - 1);
         while (nw <= upto) {
-          write(A, nw);
+          write(nw);
           ++nw;
-          if (nw < nst) issue(A, nw);
+          if (nw < nst) issue(nw);
         }
-        bar();  // B_k
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B_k
       }
     }
   } else if (wave == G::NWC) {
