@@ -290,51 +290,51 @@ __device__ __forceinline__ void corr_bwd_rows_body(const float* __restrict__ fea
     lds_barrier();
     BWD_MARK(cb == cs ? 2 : 4);  // chunk computed
     // ---- epilogue: the 9 tj partials of each (channel, pixel) summed in tj order ----
+    // Exactly one output (quad) per thread (the launcher guarantees ck * R * lw <= NT):
+    // threads past the last output redo the last one -- identical value, identical address --
+    // so the number of stores is static (l4 37.8 -> 37.0 us, l3 20.8 -> 20.3 against a
+    // runtime-counted store loop; holding the store back until the next chunk was staged
+    // measured 40.4: profiles/r03h_corr_bwd_tg.txt)
+    const int Rv = min(R, hp - r0);  // band rows inside the image (odd H: the last band)
+    const float inv_Rv = 1.f / (float)Rv;
     if (VEC) {
       const int Q = W >> 2;
-      const int nout = cn * R * Q;
-      for (int o = t; o < nout; o += NT) {
-        const int m = o - qdiv(o, g.inv_lw) * Q;  // raster quad: x = 4m .. 4m+3
-        const int rc = qdiv(o, g.inv_lw);
-        const int rr = rc - qdiv(rc, g.inv_R) * R, c = qdiv(rc, g.inv_R);
-        if (r0 + rr >= hp) continue;
-        const int i0 = 2 * m, sg = i0 >> 2, kk = i0 & 3;  // kk in {0, 2}
-        const float* p0 =
-            reinterpret_cast<const float*>(part + c * (D * RS2) + rr * 2 * g.S + sg) + kk;
-        const float* p1 = p0 + 4 * g.S;  // column parity 1
-        f32x2 e0 = *reinterpret_cast<const f32x2*>(p0);
-        f32x2 e1 = *reinterpret_cast<const f32x2*>(p1);
+      const int o = min(t, cn * Rv * Q - 1);
+      const int m = o - qdiv(o, g.inv_lw) * Q;  // raster quad: x = 4m .. 4m+3
+      const int rc = qdiv(o, g.inv_lw);
+      const int rr = rc - qdiv(rc, inv_Rv) * Rv, c = qdiv(rc, inv_Rv);
+      const int i0 = 2 * m, sg = i0 >> 2, kk = i0 & 3;  // kk in {0, 2}
+      const float* p0 =
+          reinterpret_cast<const float*>(part + c * (D * RS2) + rr * 2 * g.S + sg) + kk;
+      const float* p1 = p0 + 4 * g.S;  // column parity 1
+      f32x2 e0 = *reinterpret_cast<const f32x2*>(p0);
+      f32x2 e1 = *reinterpret_cast<const f32x2*>(p1);
 #pragma unroll
-        for (int j = 1; j < D; ++j) {
-          e0 += *reinterpret_cast<const f32x2*>(p0 + 4 * j * RS2);
-          e1 += *reinterpret_cast<const f32x2*>(p1 + 4 * j * RS2);
-        }
-        f32x4 v4 = f32x4{e0.x, e1.x, e0.y, e1.y};
-        if (inv_divisor != 0.f)
-          v4 *= inv_divisor;
-        else
-          v4 = f32x4{v4.x / divisor, v4.y / divisor, v4.z / divisor, v4.w / divisor};
-        st_out4(gin + ((size_t)n * C + cb + c) * plane + (size_t)(2 * (r0 + rr) + p) * W +
-                    4 * m,
-                v4);
+      for (int j = 1; j < D; ++j) {
+        e0 += *reinterpret_cast<const f32x2*>(p0 + 4 * j * RS2);
+        e1 += *reinterpret_cast<const f32x2*>(p1 + 4 * j * RS2);
       }
+      f32x4 v4 = f32x4{e0.x, e1.x, e0.y, e1.y};
+      if (inv_divisor != 0.f)
+        v4 *= inv_divisor;
+      else
+        v4 = f32x4{v4.x / divisor, v4.y / divisor, v4.z / divisor, v4.w / divisor};
+      st_out4(gin + ((size_t)n * C + cb + c) * plane + (size_t)(2 * (r0 + rr) + p) * W + 4 * m,
+              v4);
     } else {
-      const int nout = cn * R * W;
-      for (int o = t; o < nout; o += NT) {
-        const int x = o - qdiv(o, g.inv_lw) * W;
-        const int rc = qdiv(o, g.inv_lw);
-        const int rr = rc - qdiv(rc, g.inv_R) * R, c = qdiv(rc, g.inv_R);
-        if (r0 + rr >= hp) continue;
-        const int qq = x & 1, X = x >> 1;
-        const float* p0 = reinterpret_cast<const float*>(part + c * (D * RS2) + rr * 2 * g.S +
-                                                         qq * g.S + (X >> 2)) +
-                          (X & 3);
-        float e = *p0;
+      const int o = min(t, cn * Rv * W - 1);
+      const int x = o - qdiv(o, g.inv_lw) * W;
+      const int rc = qdiv(o, g.inv_lw);
+      const int rr = rc - qdiv(rc, inv_Rv) * Rv, c = qdiv(rc, inv_Rv);
+      const int qq = x & 1, X = x >> 1;
+      const float* p0 = reinterpret_cast<const float*>(part + c * (D * RS2) + rr * 2 * g.S +
+                                                       qq * g.S + (X >> 2)) +
+                        (X & 3);
+      float e = *p0;
 #pragma unroll
-        for (int j = 1; j < D; ++j) e += p0[4 * j * RS2];
-        e = inv_divisor != 0.f ? e * inv_divisor : e / divisor;
-        st_out1(gin + ((size_t)n * C + cb + c) * plane + (size_t)(2 * (r0 + rr) + p) * W + x, e);
-      }
+      for (int j = 1; j < D; ++j) e += p0[4 * j * RS2];
+      e = inv_divisor != 0.f ? e * inv_divisor : e / divisor;
+      st_out1(gin + ((size_t)n * C + cb + c) * plane + (size_t)(2 * (r0 + rr) + p) * W + x, e);
     }
   }
   BWD_MARK(5);  // stores issued
@@ -406,6 +406,8 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
     if (g.G == 1) return hipErrorNotSupported;
   }
   g.lw = vec ? W / 4 : W;
+  // the epilogue stores one output (quad) per thread and chunk
+  if ((long long)g.ck * R * g.lw > NT) return hipErrorNotSupported;
   g.census = debug_knob("bwd_census", 0);
   g.nld = g.ck * (R + 8) * g.lw;
   // channel slices (grid.y) up to one workgroup per CU over both gradients (grid.z): the
