@@ -55,6 +55,7 @@ import ctypes
 import json
 import os
 import platform
+import re
 import socket
 import subprocess
 import sys
@@ -77,6 +78,10 @@ CORR_ARGS = dict(pad_size=2 * SEARCH_RANGE + 1, kernel_size=1,
                  max_displacement=2 * SEARCH_RANGE + 1, stride1=1, stride2=2)  # model.py:24
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PAIR_SEED = 20240601   # synthetic pair g of the checked set is seeded PAIR_SEED + g
+# the l4-sized correlation kernels (csrc/corr_strip.hip for fp32 C = 32, corr_stream.hip else)
+L4_KERNEL_RE = "corr_fwd_str(ip|eam)"
+CORR4_ARGS = dict(pad_size=SEARCH_RANGE, kernel_size=1, max_displacement=SEARCH_RANGE,
+                  stride1=1, stride2=1)  # the north star's literal "d=4": displacements -4..4
 
 
 def level_shapes(H, W):
@@ -111,6 +116,10 @@ def parse_args(argv=None):
     ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-net-forward", action="store_true",
+                    help="skip the labelled end-to-end Net forward object (N=1 only)")
+    ap.add_argument("--no-corr4", action="store_true",
+                    help="skip the labelled Correlation(4,1,4,1,1) roofline object (N=1 only)")
     ap.add_argument("--no-graph", action="store_true", help="same as --timing eager")
     ap.add_argument("--timing", default="eager", choices=["eager", "graph-eager", "graph-all"],
                     help="eager (default): every kernel a direct C-ABI launch on pre-built "
@@ -599,7 +608,12 @@ def cpu_baseline_torch(shapes, B, seconds):
                 sample=f"median of {len(times)} passes x {B} pairs, {sum(times):.1f} s: the "
                        "reference's pure-PyTorch CPU path (WarpingLayer = grid_sample("
                        "align_corners=True) + CostVolumeLayer(sr=4), modules.py:31-74) at "
-                       f"l0-l4 of 384x448, fp32, torch.get_num_threads()={thr}")
+                       f"l0-l4 of 384x448, fp32, torch.get_num_threads()={thr}. NOTE: the "
+                       "correlation timed here is CostVolumeLayer(sr=4) (the reference's CPU "
+                       "correlation: 81 displacements -4..4 step 1, divided by 81), not the GPU "
+                       "path's Correlation(9,1,9,1,2) (81 displacements -8..8 step 2, divided by "
+                       "C): both read the same C x H x W inputs, write the same 81 x H x W "
+                       "volume and do the same 81*C multiply-adds per pixel")
 
 
 def cpu_config1(seconds):
@@ -659,6 +673,96 @@ def cpu_baseline_port(shapes, B, seconds, threads):
                        f"C port oracle/pwc_oracle.c, {used} OpenMP threads, {el:.1f} s")
 
 
+def corr4_roofline(dev, dtype, B, shape, launches=100):
+    """Secondary roofline line (labelled, not the headline): the north star's literal "d=4",
+    Correlation(pad 4, k 1, md 4, s1 1, s2 1) -- 81 displacements -4..4 step 1, the same bytes
+    and multiply-adds as model.py:24's Corr9 -- at the l4 shape, B pairs, each launch timed
+    with hipExtLaunchKernel start/stop events (pwc_time_next_corr) on buffer sets rotated past
+    the Infinity Cache, launches back to back."""
+    from pwcnet_amd import _lib
+    L = _lib.load()
+    C, h, w = shape
+    esz = 4 if dtype == torch.float32 else 2
+    P = [CORR4_ARGS[k] for k in ("pad_size", "kernel_size", "max_displacement", "stride1",
+                                 "stride2")]
+    OC, Ho, Wo = _lib.corr_output_shape(h, w, *P)
+    per = (2 * C * h * w + OC * Ho * Wo) * B * esz
+    nsets = max(2, int(np.ceil(2 * 256 * 2 ** 20 / per)))
+    gen = torch.Generator(device=dev).manual_seed(4)
+    sets = [(torch.randn(B, C, h, w, device=dev, generator=gen).to(dtype),
+             torch.randn(B, C, h, w, device=dev, generator=gen).to(dtype),
+             torch.empty(B, OC, Ho, Wo, device=dev, dtype=dtype)) for _ in range(nsets)]
+    dcode = _lib.DTYPE_CODES[dtype]
+    sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+    def launch(i, ev=None):
+        x1, x2, o = sets[i % nsets]
+        if ev is not None:
+            _lib.check(L.pwc_time_next_corr(ctypes.c_void_p(ev[0].cuda_event),
+                                            ctypes.c_void_p(ev[1].cuda_event)), "corr4")
+        _lib.check(L.pwc_corr_forward(ctypes.c_void_p(x1.data_ptr()),
+                                      ctypes.c_void_p(x2.data_ptr()),
+                                      ctypes.c_void_p(o.data_ptr()), B, C, h, w, *P, 1, dcode,
+                                      sp), "corr4")
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(launches)]
+    for a, b in evs:
+        a.record()
+        b.record()
+    for i in range(20):
+        launch(i)
+    torch.cuda.synchronize(dev)
+    for i in range(launches):
+        launch(i, evs[i])
+    torch.cuda.synchronize(dev)
+    us = float(np.mean([a.elapsed_time(b) for a, b in evs])) * 1e3
+    nbytes = corr_bytes_per_pair(C, h, w, esz) * B
+    ach = nbytes / (us * 1e-6) / 1e9
+    return {"kernel": f"l4 Correlation(4, 1, 4, 1, 1) ({C}x{h}x{w}, B={B}, "
+                      f"{'fp32' if esz == 4 else 'fp16'}): the north star's literal d=4, "
+                      f"{launches} back-to-back launches, hipExtLaunchKernel start/stop events",
+            "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes,
+            "avg_launch_us": round(us, 3)}
+
+
+def net_forward(dev, B, H, W, hot_ms, iters=5):
+    """End-to-end forward of the whole network (model.py:48-115): pwcnet_amd.net.Net at the
+    reference defaults, convs on MIOpen fp32 (out of this project's scope), the hot path on
+    the HIP drop-ins (fused forms: UpsampleWarp, CorrelationCat), random-init weights
+    (model.py:39-46 under manual_seed(0)), x ~ U[0,255) of B pairs; timed with events over
+    `iters` forwards after two warm-up forwards (MIOpen's first calls)."""
+    from pwcnet_amd.net import Net, NetArgs
+    torch.manual_seed(0)
+    net = Net(NetArgs()).to(dev).eval()
+    gen = torch.Generator(device=dev).manual_seed(5)
+    x = torch.rand(B, 3, 2, H, W, device=dev, generator=gen) * 255.0
+    with torch.no_grad():
+        for _ in range(2):
+            net(x)
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            flows, _ = net(x)
+        b.record()
+        torch.cuda.synchronize(dev)
+    ms = a.elapsed_time(b) / iters
+    ok = bool(torch.isfinite(flows[-1]).all())
+    del net, x, flows
+    torch.cuda.empty_cache()
+    return {"value": round(B / ms * 1e3, 2), "unit": "image-pairs/s", "ms_per_batch": round(ms, 3),
+            "batch": B, "iters": iters, "finite": ok,
+            "hot_path_ms_per_batch": round(hot_ms, 4),
+            "hot_path_share": round(hot_ms / ms, 4),
+            "what": "full Net forward (model.py:48-115) on 1 MI355X: feature pyramid, 5 "
+                    "estimator levels and the full-resolution context network on MIOpen fp32 "
+                    "(out of scope), warp + Correlation on the HIP drop-ins; hot_path_share = "
+                    "the headline step's ms (warp + Correlation at l0-l4, same B) / this "
+                    "forward's ms. Compare cpu_config1 (the same forward on the CPU path, B=1)"}
+
+
 def load_pmc_traffic(path):
     """HBM bytes per launch of the l4 correlation from a committed rocprofv3 PMC summary."""
     try:
@@ -687,7 +791,7 @@ def live_pmc_traffic(B, H, W, dtype, timeout=150):
     tmp = tempfile.mkdtemp(prefix="pwc_pmc_", dir="/tmp")
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         out = os.path.join(tmp, ctr)
-        cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "corr_fwd_stream", "-d", out, "-o",
+        cmd = [prof, "--pmc", ctr, "--kernel-include-regex", L4_KERNEL_RE, "-d", out, "-o",
                "run", "--output-format", "csv", "--", sys.executable,
                os.path.join(ROOT, "tools", "kbench.py"), "--levels", "4", "--ops", "corr",
                "--iters", "20", "--batch", str(B), "--height", str(H), "--width", str(W),
@@ -706,7 +810,7 @@ def live_pmc_traffic(B, H, W, dtype, timeout=150):
             for f in files:
                 if f.endswith("counter_collection.csv"):
                     for r in csv.DictReader(open(os.path.join(root, f))):
-                        if "corr_fwd_stream" in r["Kernel_Name"]:
+                        if re.search(L4_KERNEL_RE, r["Kernel_Name"]):
                             vals.append(float(r["Counter_Value"]))
         if p.returncode != 0 or not vals:
             return None, f"rocprofv3 --pmc {ctr} failed (rc {p.returncode})"
@@ -931,9 +1035,10 @@ def main(argv=None):
         workload = (f"custom: B={B} pairs/GPU, {args.height}x{args.width} {args.dtype}, warp + "
                     "Correlation(pad 9, k 1, md 9, s1 1, s2 2) at levels l0-l4")
     result = {
-        "metric": f"image-pairs/sec (forward, {args.height}x{args.width}): hot path = "
-                  "WarpingLayer + Correlation(d=4) at all 5 pyramid levels; lvl2 corr HBM GB/s "
-                  "vs peak",
+        "metric": f"image-pairs/sec (forward, {args.height}x{args.width}) at {world} MI355X: "
+                  "hot path = WarpingLayer + model.py:24's Correlation(pad 9, k 1, md 9, s1 1, "
+                  "s2 2: 81 displacements -8..8 step 2) at all 5 pyramid levels; lvl2 corr HBM "
+                  "GB/s vs peak",
         "value": round(value, 2),
         "unit": "image-pairs/s",
         "n_gpus": world,
@@ -994,6 +1099,11 @@ def main(argv=None):
             "algorithmic_bytes_per_launch": bytes_launch,
             "avg_launch_us": round(kern_ms * 1e3, 3),
         }
+    if rank == 0 and world == 1 and not cpu and not args.no_corr4:
+        result["roofline_corr4"] = corr4_roofline(dev, dtype, B, shapes[-1])
+    if rank == 0 and world == 1 and not cpu and not args.no_net_forward:
+        result["net_forward"] = net_forward(dev, B, args.height, args.width,
+                                            elapsed / args.steps * 1e3)
     if rank == 0 and world == 1 and not cpu and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_torch(shapes, B, args.cpu_seconds)
         result["cpu_baseline"]["speedup"] = round(value / result["cpu_baseline"]["value"], 1)

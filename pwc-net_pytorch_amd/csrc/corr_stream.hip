@@ -761,10 +761,20 @@ bool corr_stream_accepts(const void* in1, const void* in2, const void* out, int 
   return nblk >= 192 && W >= 64 && (s2 == 1 || s2 == 2);
 }
 
+bool corr_strip_accepts(const void*, const void*, const void*, int, int, int, int, int, int, int);
+hipError_t corr_forward_strip(const void*, const void*, void*, int, int, int, int, float,
+                              hipStream_t);
+
 hipError_t corr_forward_stream(const void* in1, const void* in2, void* out, int B, int C, int H,
                                int W, int s2, int dtype, int layout, float divisor,
                                hipStream_t stream) {
   if (!corr_stream_accepts(in1, in2, out, B, C, H, W, s2, dtype)) return hipErrorNotSupported;
+  // fp32 model-config grids of C = 32 (config 2 l4): the strip kernel (corr_strip.hip), whose
+  // stores drain under compute; it declines what it does not serve
+  if (corr_strip_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)) {
+    const hipError_t e = corr_forward_strip(in1, in2, out, B, C, H, W, divisor, stream);
+    if (e != hipErrorNotSupported) return e;
+  }
   const int twp = (W % 112 == 0 || W < 112) ? 112 : 128;  // column tile width in pixels
   using namespace stream;
 #define PWC_PICK(T)                                                                            \

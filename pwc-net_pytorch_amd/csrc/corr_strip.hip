@@ -1,0 +1,418 @@
+// corr_strip.hip — correlation forward for the l4-sized fp32 grids of model.py:24's
+// Correlation(9, 1, 9, 1, 2) (BASELINE config 2 l4: 32 x 96 x 112, B = 8): output rows are
+// produced in STEPS so that their stores drain while the next rows compute.
+//
+// Semantics (correlation_cuda_kernel.cu:34-106 with k = 1, s1 = 1, pad = md = 9, s2 = 2, C = 32):
+//   out[n, (tj+4)*9 + (ti+4), y, x] = sum_c f1[n,c,y,x] * f2[n,c,y+2tj,x+2ti] / C
+// with zeros outside the image (the reference's zero-padded scratch).
+//
+// Why this shape.  corr_stream.hip streams the channels of a 3-row band through
+// an LDS ring; every output needs the last channel, so the 28 MB of output only starts to
+// drain after the loop and ~9 us of each launch is a store phase with nothing under it.  Here a
+// workgroup owns a column STRIP (56 px) of R = 6 parity rows, and ALL channels of the R + 8 f2
+// parity rows it meets stay resident in LDS (14 rows x 32 ch x 72 px x 4 B = 129 KB).  The
+// rows are then produced two at a time in R / 2 = 3 steps: step s computes parity rows 2s and
+// 2s+1 of the strip (f2 rows 2s .. 2s+9), reduces, and issues its stores straight from the
+// registers, and step s+1 starts computing at once — its loads were staged during step s — so
+// two thirds of the output drains under compute.  Step 0's f2 rows arrive channel pair by
+// channel pair (the loader's first DMAs bring the first channels of all ten window rows), so
+// step 0 computes behind the loads the way the ring kernel does.
+//
+//   * loader wave: 14 rows x 9 LDS-DMAs (buffer_load_dwordx4 ... lds, 1 KiB each; the buffer
+//     range check gives the zero border), <= 63 in flight, one s_barrier per landed group.
+//   * compute waves: two quads of four (quad q takes parity rows 2s + q); lane = (tj, 4-px
+//     segment, channel half): per channel 5 ds_read_b128 of the f2 window and 18 v_pk_fma_f32
+//     on f1 values held in registers (loaded by the lane itself, the next step's f1 prefetched
+//     into the register of the channel just consumed).  The two channel halves of a task sit in
+//     lanes l and l+32 and are summed by v_permlane32_swap (one swap + one add per accumulator
+//     pair).  9 tj x 14 segments = 126 tasks -> 4 waves of 32 task slots per quad.
+//   * LDS rows are 590 quads apart (= 14 mod 16): every ds_read_b128 lane group of the lane map
+//     hits 16 distinct 16-B bank slots (conflict-free; checked by tools/strip_conflicts.py).
+//   * stores: 16 B per lane (4 px of one displacement plane), consecutive segments in
+//     consecutive lanes (224-B runs), nontemporal; 5 (low half) / 4 (high half) per step.
+//   * blocks are remapped XCD-aware so the strips of one image parity share an L2 (their f2
+//     rows overlap between row groups and at the strip halo).
+#include <hip/hip_ext.h>
+
+#include <cmath>
+#include <type_traits>
+
+#include "pwc_common.cuh"
+
+namespace pwc {
+
+void take_launch_events(hipEvent_t* start, hipEvent_t* stop);  // capi.hip
+
+namespace strip {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int C_, int R_, int TW_>
+struct Geo {
+  static constexpr int C = C_, R = R_, TW = TW_;
+  static constexpr int CH = C / 2;          // channels per lane half
+  static constexpr int NSEG = TW / 4;       // 4-px segments per strip row
+  static constexpr int QR = (TW + 16) / 4;  // quads per staged channel row (8-px halo each side)
+  static constexpr int ROWQ = C * QR;       // quads per staged f2 row (all channels)
+  static constexpr int IPR = ROWQ / 64;     // LDS-DMAs per f2 row
+  // row stride in quads: = 14 (mod 16) makes the lane map's ds_read_b128 groups conflict-free
+  static constexpr int SIGMA = ROWQ + ((14 - ROWQ % 16) + 16) % 16;
+  static constexpr int NROW = R + 8;        // f2 parity rows of the strip
+  static constexpr int NQD = 2;             // compute quads (rows per step)
+  static constexpr int NSTEP = R / NQD;
+  static constexpr int WIN = NQD + 8;       // f2 rows of step 0
+  static constexpr int NTASK = 9 * NSEG;    // (tj, segment) tasks per output row
+  static constexpr int WPP = (NTASK + 31) / 32;  // waves per quad (32 task slots each)
+  static constexpr int NWC = WPP * NQD;     // compute waves
+  static constexpr int THREADS = 64 * (NWC + 1);
+  static constexpr int LDS_BYTES = NROW * SIGMA * 16;
+  static constexpr int NDMA = NROW * IPR;
+  static constexpr int NBAR = IPR + NSTEP - 1;  // barriers every wave executes
+  static_assert(C % 2 == 0 && TW % 4 == 0 && R % NQD == 0, "geometry");
+  static_assert(ROWQ % 64 == 0, "a staged row is whole DMAs");
+  static_assert(LDS_BYTES <= 160 * 1024 && THREADS <= 1024, "workgroup resources");
+  // every read offset is an instruction immediate (16-bit)
+  static_assert(((NSTEP - 1) * NQD * SIGMA + (C - 2) * QR + 4) * 16 < 65536, "ds offsets");
+};
+
+// Loader DMA d -> (f2 row m, DMA i of the row): step 0's ten rows group-major (group i of all
+// rows before group i + 1), then the later rows whole.
+template <class G>
+constexpr int dma_row(int d) {
+  return d < G::IPR * G::WIN ? d % G::WIN : G::WIN + (d - G::IPR * G::WIN) / G::IPR;
+}
+template <class G>
+constexpr int dma_idx(int d) {
+  return d < G::IPR * G::WIN ? d / G::WIN : (d - G::IPR * G::WIN) % G::IPR;
+}
+// DMAs that have landed before barrier j: group j of step 0's rows (j < IPR), then every row
+// of step s = j - IPR + 1.
+template <class G>
+constexpr int dma_need(int j) {
+  return j < G::IPR ? (j + 1) * G::WIN : G::IPR * (G::WIN + G::NQD * (j - G::IPR + 1));
+}
+// DMAs issued before barrier j's wait: never more than 63 in flight (the 6-bit vmcnt), counting
+// every DMA not yet known to have landed (those before barrier j-1's wait are)
+template <class G>
+constexpr int dma_target(int j) {
+  return (j > 0 ? dma_need<G>(j - 1) : 0) + 63 < G::NDMA ? (j > 0 ? dma_need<G>(j - 1) : 0) + 63
+                                                         : G::NDMA;
+}
+// DMA group that completes channel pair k (LDS channel rows 2k, 2k+1)
+template <class G>
+constexpr int pair_group(int k) {
+  return ((2 * k + 2) * G::QR - 1) / 64;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One row of the loader: the buffer resource starts at the row (zero records for a row
+// outside the image: the whole DMA reads zeros).
+struct RowRsrc {
+  const float* img;
+  uint32_t img_bytes, row_bytes;
+  int Y0, py, H;
+};
+
+template <class G, int D>
+__device__ __forceinline__ void dma_one(const RowRsrc& rr, const uint32_t (&rel)[G::IPR],
+                                        uint32_t lds0) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int m = dma_row<G>(D), i = dma_idx<G>(D);
+  const int pr = rr.Y0 - 4 + m;            // parity row of the image
+  const int yrow = 2 * pr + rr.py;         // image row
+  const bool ok = pr >= 0 && yrow < rr.H;
+  const uint32_t off = ok ? (uint32_t)yrow * rr.row_bytes : 0u;
+  const int nrec = ok ? (int)(rr.img_bytes - off) : 0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)rr.img + off), (short)0, nrec, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      rs, (__attribute__((address_space(3))) void*)(uintptr_t)(lds0 + (uint32_t)((m * G::SIGMA + 64 * i) * 16)),
+      16, rel[i], 0, 0, 0);
+#endif
+}
+
+template <class G, int D, int E>
+__device__ __forceinline__ void dma_range(const RowRsrc& rr, const uint32_t (&rel)[G::IPR],
+                                          uint32_t lds0) {
+  if constexpr (D < E) {
+    dma_one<G, D>(rr, rel, lds0);
+    dma_range<G, D + 1, E>(rr, rel, lds0);
+  }
+}
+
+// Barrier j of the loader: issue up to dma_target(j), wait for dma_need(j), barrier.
+template <class G, int J>
+__device__ __forceinline__ void loader_from(const RowRsrc& rr, const uint32_t (&rel)[G::IPR],
+                                            uint32_t lds0) {
+  if constexpr (J < G::NBAR) {
+    constexpr int from = J == 0 ? 0 : dma_target<G>(J - 1);
+    constexpr int to = dma_target<G>(J);
+    static_assert(to >= dma_need<G>(J) && to - dma_need<G>(J) <= 63, "DMA schedule");
+    dma_range<G, from, to>(rr, rel, lds0);
+    wait_vmcnt<to - dma_need<G>(J)>();
+    __builtin_amdgcn_s_barrier();
+    loader_from<G, J + 1>(rr, rel, lds0);
+  }
+}
+
+// Five ds_read_b128 of one channel's f2 window (immediate offset O).
+template <int O>
+__device__ __forceinline__ void read5(uint32_t a, f32x4 (&w)[5]) {
+  static_assert(O >= 0 && O + 64 < 65536, "ds offset field");
+  asm volatile(
+      "ds_read_b128 %0, %5 offset:%6\n\t"
+      "ds_read_b128 %1, %5 offset:%7\n\t"
+      "ds_read_b128 %2, %5 offset:%8\n\t"
+      "ds_read_b128 %3, %5 offset:%9\n\t"
+      "ds_read_b128 %4, %5 offset:%10"
+      : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4])
+      : "v"(a), "n"(O), "n"(O + 16), "n"(O + 32), "n"(O + 48), "n"(O + 64)
+      : "memory");
+}
+
+// Wait until at most N LDS reads are outstanding; the window registers it completes are tied
+// through the asm so the compiler neither reads them earlier nor reuses them meanwhile.
+template <int N>
+__device__ __forceinline__ void lgk_wait(f32x4 (&w)[5]) {
+  asm volatile("s_waitcnt lgkmcnt(%5)"
+               : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4])
+               : "n"(N));
+}
+
+// v_permlane32_swap_b32 a, b: a's lanes 32-63 <-> b's lanes 0-31.  Written as asm: with ROCm
+// 7.2 the builtin's two results fold into one register when both feed one add (the sum read
+// v + v), dropping the other half.  The s_nops cover the VALU -> permlane operand hazard on
+// either side.
+__device__ __forceinline__ void swap32(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+}
+
+struct LaneCtx {
+  uint32_t addr;                   // LDS byte address of (row qd + tj, channel half, segment)
+  __amdgpu_buffer_rsrc_t rs1;      // f1 of this image
+  uint32_t f1off;                  // f1 voffset of step 0 (or kOOB)
+  uint32_t f1step;                 // f1 voffset increment per step
+  uint32_t plane_b;                // channel plane bytes
+  int nstep_ok;                    // steps whose output row exists
+};
+
+constexpr uint32_t kOOB = 0x80000000u;
+
+template <class G>
+__device__ __forceinline__ f32x4 load_f1(const LaneCtx& lc, int st, int k) {
+  const uint32_t v = st < lc.nstep_ok && lc.f1off != kOOB ? lc.f1off + (uint32_t)st * lc.f1step
+                                                          : kOOB;
+  return __builtin_bit_cast(
+      f32x4, __builtin_amdgcn_raw_buffer_load_b128(lc.rs1, (int)v, (int)(k * lc.plane_b), 0));
+}
+
+// Channel k of step ST: barrier (step 0, when pair k+1 opens a DMA group), the next channel's
+// window reads, this channel's FMAs, the next step's f1 prefetch into f1[k].
+template <class G, int ST, int K>
+__device__ __forceinline__ void channel(const LaneCtx& lc, float (&acc)[9][4], f32x4 (&f1)[G::CH],
+                                        f32x4 (&wA)[5], f32x4 (&wB)[5]) {
+  if constexpr (K < G::CH) {
+    f32x4(&cur)[5] = (K & 1) ? wB : wA;
+    f32x4(&nxt)[5] = (K & 1) ? wA : wB;
+    if constexpr (K + 1 < G::CH) {
+      if constexpr (ST == 0 && pair_group<G>(K + 1) > pair_group<G>(K))
+        __builtin_amdgcn_s_barrier();
+      constexpr int O = (ST * G::NQD * G::SIGMA + 2 * (K + 1) * G::QR) * 16;
+      read5<O>(lc.addr, nxt);
+      lgk_wait<5>(cur);
+    } else {
+      lgk_wait<0>(cur);
+    }
+    corr_fma_pairs_s2<9, 5>(acc, f1[K], cur);
+    if constexpr (ST + 1 < G::NSTEP) f1[K] = load_f1<G>(lc, ST + 1, K);
+    __builtin_amdgcn_sched_barrier(0);
+    channel<G, ST, K + 1>(lc, acc, f1, wA, wB);
+  }
+}
+
+template <class G>
+__global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
+    const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
+    int H, int W, int ngrp, int ntx, float inv_divisor, OutEpi epi) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  // logical block = (n, row parity, row group, strip), strip fastest: the strips of one image
+  // parity are neighbours and xcd_remap keeps neighbours on one XCD (shared f2 rows)
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tx = t % ntx;
+  const int grp = (t / ntx) % ngrp;
+  const int py = (t / (ntx * ngrp)) & 1;
+  const int n = t / (ntx * ngrp * 2);
+  const int Y0 = grp * G::R;  // first parity row of the group
+  const int x0 = tx * G::TW;  // first pixel of the strip
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t plane_b = (uint32_t)(H * W) * 4u;
+  const uint32_t img_bytes = (uint32_t)G::C * plane_b;  // < 2^31 (launcher)
+  const float* img1 = in1 + (size_t)n * G::C * H * W;
+  const float* img2 = in2 + (size_t)n * G::C * H * W;
+  const uint32_t lds0 = lds_addr(lds);
+
+  if (wave == G::NWC) {
+    // ---------------- loader wave ----------------
+    uint32_t rel[G::IPR];
+#pragma unroll
+    for (int i = 0; i < G::IPR; ++i) {
+      const int qq = 64 * i + lane;            // quad of the staged row
+      const int l = qq / G::QR, qx = qq % G::QR;  // LDS channel row, quad in it
+      const int c = (l >> 1) + G::CH * (l & 1);   // channel pairs (c, c + C/2) adjacent
+      const int px = x0 - 8 + 4 * qx;
+      rel[i] = px >= 0 && px < W ? ((uint32_t)c * plane_b + (uint32_t)px * 4u) : kOOB;
+    }
+    const RowRsrc rr{img2, img_bytes, (uint32_t)W * 4u, Y0, py, H};
+    loader_from<G, 0>(rr, rel, lds0);
+    return;
+  }
+
+  // ---------------- compute waves ----------------
+  const int qd = wave / G::WPP, wq = wave % G::WPP;
+  const int slot = lane & 31, chalf = lane >> 5;
+  const int task = 32 * wq + slot;
+  const bool active = task < G::NTASK;
+  const int tt = active ? task : G::NTASK - 1;  // idle slots duplicate a lane of their group
+  const int tj = tt / G::NSEG, seg = tt % G::NSEG;
+  const int px = x0 + 4 * seg;
+  LaneCtx lc;
+  lc.addr = lds0 + (uint32_t)(((qd + tj) * G::SIGMA + chalf * G::QR + seg) * 16);
+  lc.rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)img1, (short)0, (int)img_bytes, 0x00020000);
+  const int yrow0 = 2 * (Y0 + qd) + py;  // this quad's output row in step 0
+  lc.f1off = px < W ? ((uint32_t)(chalf * G::CH) * plane_b + ((uint32_t)yrow0 * W + px) * 4u)
+                    : kOOB;
+  lc.f1step = (uint32_t)(2 * G::NQD * W) * 4u;
+  lc.plane_b = plane_b;
+  // steps whose output row (2 (Y0 + 2 st + qd) + py) lies inside the image
+  lc.nstep_ok = yrow0 < H ? min(G::NSTEP, (H - 1 - yrow0) / (2 * G::NQD) + 1) : 0;
+
+  f32x4 f1[G::CH];
+#pragma unroll
+  for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, 0, k);
+
+  // output: one buffer resource over the image's 81 planes; a store whose lane has nothing to
+  // write (idle task, row or strip outside the image, the high half's fifth store) gets an
+  // out-of-range offset.  Every store instruction is then unconditional, so the compiler's
+  // vmcnt count for the f1 prefetch stays exact across steps (a branch around a store makes
+  // it assume the store-less path and wait for stores still draining).
+  float* oimg = out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * H * W);
+  const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)oimg, (short)0, (int)(81u * plane_b), 0x00020000);
+  // leaky_relu (model.py:84) as max(v, slope v): equal to epi_act for slope <= 1 (the
+  // launcher declines larger slopes), and the identity at slope 1, bit for bit
+  const float slope = epi.slope;
+  auto step = [&](auto st_c) {
+    constexpr int ST = decltype(st_c)::value;
+    float acc[9][4];
+#pragma unroll
+    for (int a = 0; a < 9; ++a)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[a][e] = 0.f;
+    f32x4 wA[5], wB[5];
+    __builtin_amdgcn_s_barrier();  // step 0: group 0 landed; later steps: their rows landed
+    read5<ST * G::NQD * G::SIGMA * 16>(lc.addr, wA);
+    channel<G, ST, 0>(lc, acc, f1, wA, wB);
+    // channel halves: lane l (c < C/2) and l + 32 (c >= C/2) hold partial sums of the same
+    // task.  One v_permlane32_swap per pair (ti, ti + 5) leaves both halves of the pair in
+    // each lane; their sum is displacement ti's total in one half and ti + 5's in the other.
+    float res[5][4];
+#pragma unroll
+    for (int ti = 0; ti < 5; ++ti)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = acc[ti][e], b = ti < 4 ? acc[ti + 5][e] : acc[ti][e];
+        swap32(a, b);
+        res[ti][e] = a + b;
+      }
+    const int yrow = yrow0 + 2 * G::NQD * ST;
+    const bool wr = active && px < W && ST < lc.nstep_ok;
+    // the swap pairs (ti, ti + 5): the low half keeps ti, the high half ti + 5
+    const uint32_t o0 = (uint32_t)(((tj * 9 + 5 * chalf) * H + yrow) * W + px) * 4u;
+    const uint32_t ostep = plane_b;  // next displacement plane
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float o = res[q][e] * inv_divisor;  // exact: the divisor is a power of two
+        v[e] = __builtin_bit_cast(uint32_t, fmaxf(o, o * slope));
+      }
+      const bool ok = wr && (q < 4 || chalf == 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0,
+                                             2 /* nt */);
+    }
+  };
+  step(std::integral_constant<int, 0>{});
+  if constexpr (G::NSTEP > 1) step(std::integral_constant<int, 1>{});
+  if constexpr (G::NSTEP > 2) step(std::integral_constant<int, 2>{});
+  static_assert(G::NSTEP <= 3, "unrolled steps");
+}
+
+template <class G>
+static hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int W,
+                         float divisor, hipStream_t stream) {
+  const int hp0 = (H + 1) / 2;  // parity-0 rows (the larger parity)
+  const int ngrp = (hp0 + G::R - 1) / G::R;
+  const int ntx = (W + G::TW - 1) / G::TW;
+  const long long nblk = (long long)B * 2 * ngrp * ntx;
+  if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_strip<G>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  int ex;
+  const float m = std::frexp(divisor, &ex);
+  if (m != 0.5f) return hipErrorNotSupported;  // the epilogue multiplies by 1 / divisor exactly
+  const float inv = std::ldexp(1.f, 1 - ex);
+  const OutEpi epi = current_epi();
+  if (!(epi.slope <= 1.f)) return hipErrorNotSupported;  // max(v, slope v) form
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
+  hipExtLaunchKernelGGL((corr_fwd_strip<G>), dim3((unsigned)nblk), dim3(G::THREADS),
+                        G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,
+                        (float*)out, H, W, ngrp, ntx, inv, epi);
+  return hipGetLastError();
+}
+
+using GeoL4 = Geo<32, 6, 56>;
+
+}  // namespace strip
+
+// Whether the strip kernel serves this problem: fp32, model.py:24's stride-2 displacements in
+// raster order (dr = 4, pad = md, k = 1, s1 = 1: checked by the caller), C = 32, W a multiple
+// of the 56-px strip, 16-B aligned buffers, and at least about one workgroup per CU (smaller
+// grids leave CUs idle: the stream kernel's 3-row bands suit them better).  Knob strip=0
+// disables it (measurement of the stream kernel).
+bool corr_strip_accepts(const void* in1, const void* in2, const void* out, int B, int C, int H,
+                        int W, int s2, int dtype, int layout) {
+  using G = strip::GeoL4;
+  if (dtype != 0 || s2 != 2 || layout != kRaster || C != G::C) return false;
+  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16) return false;
+  if (W % G::TW || H < 2 || (size_t)C * H * W * 4 >= 0x7ffffff0ull) return false;
+  if (debug_knob("strip", 1) == 0) return false;
+  const long long nblk = (long long)B * 2 * (((H + 1) / 2 + G::R - 1) / G::R) * (W / G::TW);
+  return nblk >= 192;
+}
+
+hipError_t corr_forward_strip(const void* in1, const void* in2, void* out, int B, int C, int H,
+                              int W, float divisor, hipStream_t stream) {
+  if (!corr_strip_accepts(in1, in2, out, B, C, H, W, 2, 0, kRaster)) return hipErrorNotSupported;
+  return strip::launch<strip::GeoL4>(in1, in2, out, B, H, W, divisor, stream);
+}
+
+}  // namespace pwc
