@@ -45,6 +45,30 @@ void take_launch_events(hipEvent_t* start, hipEvent_t* stop);  // capi.hip
 
 namespace strip {
 
+#ifdef PWC_STRIP_CENSUS  // tools/strip_bench.hip only: per-workgroup phase stamps (100 MHz)
+// Stamps are kept in scalar registers and written once at the end of the wave: a global store
+// inside the loop would enter the compute waves' vmcnt accounting and distort the timing.
+__device__ unsigned long long* g_census;
+#define STAMP(slot) (cen_t[(slot)] = __builtin_amdgcn_s_memrealtime())
+#define CENSUS_DECL unsigned long long cen_t[10] = {}
+#define CENSUS_FLUSH(lo, hi)                                                           \
+  do {                                                                                 \
+    if ((threadIdx.x & 63) == 0 && g_census != nullptr)                                \
+      for (int k_ = (lo); k_ < (hi); ++k_)                                             \
+        if (cen_t[k_]) g_census[blockIdx.x * 16 + k_] = cen_t[k_];                     \
+  } while (0)
+#else
+#define STAMP(slot) \
+  do {              \
+  } while (0)
+#define CENSUS_DECL \
+  do {              \
+  } while (0)
+#define CENSUS_FLUSH(lo, hi) \
+  do {                       \
+  } while (0)
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int C_, int R_, int TW_>
@@ -119,6 +143,9 @@ struct RowRsrc {
   const float* img;
   uint32_t img_bytes, row_bytes;
   int Y0, py, H;
+#ifdef PWC_STRIP_CENSUS
+  unsigned long long* cen;
+#endif
 };
 
 template <class G, int D>
@@ -158,6 +185,10 @@ __device__ __forceinline__ void loader_from(const RowRsrc& rr, const uint32_t (&
     static_assert(to >= dma_need<G>(J) && to - dma_need<G>(J) <= 63, "DMA schedule");
     dma_range<G, from, to>(rr, rel, lds0);
     wait_vmcnt<to - dma_need<G>(J)>();
+#ifdef PWC_STRIP_CENSUS
+    if constexpr (J == G::IPR - 1) rr.cen[8] = __builtin_amdgcn_s_memrealtime();  // window
+    if constexpr (J == G::NBAR - 1) rr.cen[9] = __builtin_amdgcn_s_memrealtime();  // all rows
+#endif
     __builtin_amdgcn_s_barrier();
     loader_from<G, J + 1>(rr, rel, lds0);
   }
@@ -259,6 +290,8 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
   const float* img1 = in1 + (size_t)n * G::C * H * W;
   const float* img2 = in2 + (size_t)n * G::C * H * W;
   const uint32_t lds0 = lds_addr(lds);
+  CENSUS_DECL;
+  STAMP(0);
 
   if (wave == G::NWC) {
     // ---------------- loader wave ----------------
@@ -271,8 +304,13 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
       const int px = x0 - 8 + 4 * qx;
       rel[i] = px >= 0 && px < W ? ((uint32_t)c * plane_b + (uint32_t)px * 4u) : kOOB;
     }
+#ifdef PWC_STRIP_CENSUS
+    const RowRsrc rr{img2, img_bytes, (uint32_t)W * 4u, Y0, py, H, cen_t};
+#else
     const RowRsrc rr{img2, img_bytes, (uint32_t)W * 4u, Y0, py, H};
+#endif
     loader_from<G, 0>(rr, rel, lds0);
+    CENSUS_FLUSH(8, 10);
     return;
   }
 
@@ -319,8 +357,10 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
       for (int e = 0; e < 4; ++e) acc[a][e] = 0.f;
     f32x4 wA[5], wB[5];
     __builtin_amdgcn_s_barrier();  // step 0: group 0 landed; later steps: their rows landed
+    if (ST == 0) STAMP(1);
     read5<ST * G::NQD * G::SIGMA * 16>(lc.addr, wA);
     channel<G, ST, 0>(lc, acc, f1, wA, wB);
+    STAMP(2 + 2 * ST);  // loop done
     // channel halves: lane l (c < C/2) and l + 32 (c >= C/2) hold partial sums of the same
     // task.  One v_permlane32_swap per pair (ti, ti + 5) leaves both halves of the pair in
     // each lane; their sum is displacement ti's total in one half and ti + 5's in the other.
@@ -351,11 +391,13 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
       __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0,
                                              2 /* nt */);
     }
+    STAMP(3 + 2 * ST);  // stores issued
   };
   step(std::integral_constant<int, 0>{});
   if constexpr (G::NSTEP > 1) step(std::integral_constant<int, 1>{});
   if constexpr (G::NSTEP > 2) step(std::integral_constant<int, 2>{});
   static_assert(G::NSTEP <= 3, "unrolled steps");
+  if (wave == 0) CENSUS_FLUSH(0, 8);
 }
 
 template <class G>

@@ -617,12 +617,13 @@ hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int
   // 16.2, l2 9.2 -> 8.4 (profiles/r02e_warp_fp16_cfg.txt); fp32 on large grids: 8 channels per
   // thread (config-2 l3 5.57 -> 5.32 us, l4 equal; l2 stays at 4: 3.52 against 3.68 --
   // profiles/r02e_warp_fp32_cfg.txt).  Other shapes measured in round 2 were removed.
-  if (npix >= 16384 && sizeof(T) == 2)
-    PWC_WARP_LAUNCH(2, 4, true);
-  else if (npix >= 16384)
-    PWC_WARP_LAUNCH(8, 1, true);
-  else
+  // (if constexpr: a variant the storage type never takes is not instantiated)
+  if (npix < 16384)
     PWC_WARP_LAUNCH(4, 1, true);
+  else if constexpr (sizeof(T) == 2)
+    PWC_WARP_LAUNCH(2, 4, true);
+  else
+    PWC_WARP_LAUNCH(8, 1, true);
 #undef PWC_WARP_LAUNCH
   return hipGetLastError();
 }
@@ -670,7 +671,7 @@ hipError_t warp_forward_group_t(const WarpProblem* probs, int count, hipStream_t
     a.n = n;
     if (!cb8)
       hipLaunchKernelGGL((warp_fwd_group<T, 4, 1>), dim3(total), dim3(256), 0, stream, a);
-    else if (sizeof(T) == 4)
+    else if constexpr (sizeof(T) == 4)
       hipLaunchKernelGGL((warp_fwd_group<T, 8, 1>), dim3(total), dim3(256), 0, stream, a);
     else
       hipLaunchKernelGGL((warp_fwd_group<T, 2, 4>), dim3(total), dim3(256), 0, stream, a);

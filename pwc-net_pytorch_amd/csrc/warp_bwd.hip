@@ -54,6 +54,8 @@ struct Args {
 __device__ unsigned long long g_wbwd_census[4096 * 16];
 // (a branch-free buffer store: a conditional store would cost the chunk loop its precise
 // vmcnt waits -- see warp_bwd_tile)
+// Product builds compile the marks and the ablation bits out (`make CENSUS=1` keeps them).
+#ifdef PWC_CENSUS
 #define WB_MARK(k)                                                                          \
   do {                                                                                      \
     const bool on_ = a.census && threadIdx.x == 0 && blockIdx.x < 4096;                     \
@@ -62,6 +64,13 @@ __device__ unsigned long long g_wbwd_census[4096 * 16];
         __builtin_bit_cast(u32x2_t, ts_), census_rsrc(),                                    \
         on_ ? (int)((blockIdx.x * 16 + (k)) * 8) : (int)0x80000000, 0, 0);                  \
   } while (0)
+#define WB_ABL(bit) (a.census & (bit))
+#else
+#define WB_MARK(k) \
+  do {             \
+  } while (0)
+#define WB_ABL(bit) 0
+#endif
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t census_rsrc() {
   return __builtin_amdgcn_make_buffer_rsrc((void*)g_wbwd_census, (short)0,
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(NT, 2) void warp_bwd_tile(Args a) {
 #pragma unroll
     for (int c = 0; c < CC; ++c) {
       const int ch = cb + c;
-      const bool ok = ch < ce && rowok && !(a.census & 2);
+      const bool ok = ch < ce && rowok && !WB_ABL(2);
       if (V4) {  // W % 4 == 0 and wx0 % 4 == 0: a quad is wholly inside or outside the row
         const unsigned off = ok && sx >= 0 && sx < W
                                  ? ((unsigned)ch * plane + (unsigned)(sy * W + sx)) * 4u
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(NT, 2) void warp_bwd_tile(Args a) {
     float acc[HC];
 #pragma unroll
     for (int c = 0; c < HC; ++c) acc[c] = 0.f;
-    const int lenx = (a.census & 4) ? 0 : len;
+    const int lenx = WB_ABL(4) ? 0 : len;
 #pragma unroll
     for (int j = 0; j < KE; ++j)
       if (j < lenx) {
@@ -319,7 +328,7 @@ __global__ __launch_bounds__(NT, 2) void warp_bwd_tile(Args a) {
 #pragma unroll
     for (int c = 0; c < HC; ++c) {  // branch-free: off-image pixels / past-group channels drop
       const int ch = cb + c0 + c;
-      const unsigned off = own && ch < ce && !(a.census & 8)
+      const unsigned off = own && ch < ce && !WB_ABL(8)
                                ? ((unsigned)ch * plane + opix) * 4u : kOOB;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[c]), rsgx, (int)off, 0, 0);
     }
@@ -456,6 +465,8 @@ struct Plan {
 static bool plan(int B, int C, int H, int W, Plan* p) {
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return false;
   if ((size_t)B * H * W * 4 >= (1ull << 31) || (size_t)B * C * H * W >= (1ull << 31)) return false;
+  // the tile kernel's buffer resources cover one image in 32-bit byte counts
+  if ((size_t)C * H * W * 4 >= (1ull << 31)) return false;
   p->ntx = (W + TS - 1) / TS;
   p->ntiles = p->ntx * ((H + TS - 1) / TS);
   const long long tiles = (long long)B * p->ntiles;
@@ -494,9 +505,17 @@ extern "C" __attribute__((visibility("default"))) int pwc_debug_wbwd_census(void
                              sizeof(unsigned long long) * (size_t)n) == hipSuccess;
 }
 
+// The tile path's choice (warp_backward_tiles_f32): wide images by default; knob
+// warp_bwd_tiles = 0 never, 2 always.
+static bool tiles_wanted(int W) {
+  const int mode = debug_knob("warp_bwd_tiles", 1);
+  return !(mode == 0 || (mode == 1 && W < 96));
+}
+
+// 0 whenever the tile path would decline, so the narrow levels pass no workspace
 size_t warp_backward_workspace_size(int B, int C, int H, int W) {
   wbwd::Plan p;
-  return wbwd::plan(B, C, H, W, &p) ? p.bytes : 0;
+  return tiles_wanted(W) && wbwd::plan(B, C, H, W, &p) ? p.bytes : 0;
 }
 
 // hipErrorNotSupported: no plan (or no workspace) -- the caller runs warp_backward_f32.
@@ -508,8 +527,7 @@ hipError_t warp_backward_tiles_f32(const void* x, const void* flow, const void* 
   // l3 equal, l2..l0 slower (the tile workgroup's list build + per-chunk barriers are a fixed
   // latency that the multi-kernel path does not pay) -- wide images only by default; knob
   // warp_bwd_tiles = 0 never, 2 always (tests)
-  const int mode = debug_knob("warp_bwd_tiles", 1);
-  if (mode == 0 || (mode == 1 && W < 96)) return hipErrorNotSupported;
+  if (!tiles_wanted(W)) return hipErrorNotSupported;
   Plan p;
   if (!plan(B, C, H, W, &p) || ws == nullptr || ws_bytes < p.bytes) return hipErrorNotSupported;
   char* w = (char*)ws;

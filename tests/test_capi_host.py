@@ -72,6 +72,19 @@ def test_error_paths_return_zero_with_message():
     assert b"empty" in lib.pwc_last_error()
     # warp backward is fp32 only
     assert lib.pwc_warp_backward(one, one, one, one, one, 1, 1, 4, 4, 1, null) == 0
+    # ABI 8's workspace form: the same checks, and no workspace asked for where the tile path
+    # declines (narrow images) or for a bad dtype / negative dims
+    assert lib.pwc_warp_backward_ws(one, one, one, one, one, 1, 1, 4, 4, 1, null, 0, null) == 0
+    assert b"fp32 only" in lib.pwc_last_error()
+    assert lib.pwc_warp_backward_ws(null, null, null, null, null, 1, 1, 4, 4, 0, null, 0,
+                                    null) == 0
+    assert b"null" in lib.pwc_last_error()
+    assert lib.pwc_warp_backward_ws(one, one, one, one, one, 1, 1, -4, 4, 0, null, 0, null) == 0
+    assert b"negative" in lib.pwc_last_error()
+    assert lib.pwc_warp_backward_workspace_size(8, 32, 96, 112, 1) == 0      # fp16
+    assert lib.pwc_warp_backward_workspace_size(8, 32, -96, 112, 0) == 0     # negative dim
+    assert lib.pwc_warp_backward_workspace_size(8, 64, 48, 56, 0) == 0       # l3: multi-kernel
+    assert lib.pwc_warp_backward_workspace_size(8, 32, 96, 112, 0) > 0       # l4: tile path
     with pytest.raises(RuntimeError, match="aborting"):
         _lib.check(0, "x")
 

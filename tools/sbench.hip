@@ -2,7 +2,7 @@
 // (csrc/corr_stream.hip), no torch.  Per launch: hipExtLaunchKernel event time; per
 // workgroup: s_memrealtime at start, loader's last landing, loop end, parked, stores issued.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPWC_STREAM_CENSUS -o tools/sbench tools/sbench.hip
-//   PWC_DEBUG=stream_cfg=..,stream_abl=.. tools/sbench [iters]
+//   PWC_DEBUG=stream_abl=.. tools/sbench [iters]
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
