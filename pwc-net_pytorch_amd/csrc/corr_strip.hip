@@ -50,12 +50,12 @@ namespace strip {
 // inside the loop would enter the compute waves' vmcnt accounting and distort the timing.
 __device__ unsigned long long* g_census;
 #define STAMP(slot) (cen_t[(slot)] = __builtin_amdgcn_s_memrealtime())
-#define CENSUS_DECL unsigned long long cen_t[10] = {}
-#define CENSUS_FLUSH(lo, hi)                                                           \
+#define CENSUS_DECL unsigned long long cen_t[16] = {}
+#define CENSUS_FLUSH(lo, hi, base)                                                     \
   do {                                                                                 \
     if ((threadIdx.x & 63) == 0 && g_census != nullptr)                                \
       for (int k_ = (lo); k_ < (hi); ++k_)                                             \
-        if (cen_t[k_]) g_census[blockIdx.x * 16 + k_] = cen_t[k_];                     \
+        if (cen_t[k_]) g_census[blockIdx.x * 32 + (base) + k_] = cen_t[k_];            \
   } while (0)
 #else
 #define STAMP(slot) \
@@ -64,7 +64,7 @@ __device__ unsigned long long* g_census;
 #define CENSUS_DECL \
   do {              \
   } while (0)
-#define CENSUS_FLUSH(lo, hi) \
+#define CENSUS_FLUSH(lo, hi, base) \
   do {                       \
   } while (0)
 #endif
@@ -186,8 +186,9 @@ __device__ __forceinline__ void loader_from(const RowRsrc& rr, const uint32_t (&
     dma_range<G, from, to>(rr, rel, lds0);
     wait_vmcnt<to - dma_need<G>(J)>();
 #ifdef PWC_STRIP_CENSUS
-    if constexpr (J == G::IPR - 1) rr.cen[8] = __builtin_amdgcn_s_memrealtime();  // window
-    if constexpr (J == G::NBAR - 1) rr.cen[9] = __builtin_amdgcn_s_memrealtime();  // all rows
+    if constexpr (J == 0) rr.cen[13] = __builtin_amdgcn_s_memrealtime();  // group 0
+    if constexpr (J == G::IPR - 1) rr.cen[14] = __builtin_amdgcn_s_memrealtime();  // window
+    if constexpr (J == G::NBAR - 1) rr.cen[15] = __builtin_amdgcn_s_memrealtime();  // all rows
 #endif
     __builtin_amdgcn_s_barrier();
     loader_from<G, J + 1>(rr, rel, lds0);
@@ -224,6 +225,19 @@ __device__ __forceinline__ void lgk_wait(f32x4 (&w)[5]) {
 // either side.
 __device__ __forceinline__ void swap32(float& a, float& b) {
   asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+}
+// Four swaps in one block: one s_nop pair covers them (no swap reads a register another
+// writes).
+__device__ __forceinline__ void swap32x4(float& a0, float& b0, float& a1, float& b1, float& a2,
+                                         float& b2, float& a3, float& b3) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_permlane32_swap_b32 %0, %1\n\t"
+      "v_permlane32_swap_b32 %2, %3\n\t"
+      "v_permlane32_swap_b32 %4, %5\n\t"
+      "v_permlane32_swap_b32 %6, %7\n\t"
+      "s_nop 1"
+      : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3));
 }
 
 struct LaneCtx {
@@ -269,7 +283,7 @@ __device__ __forceinline__ void channel(const LaneCtx& lc, float (&acc)[9][4], f
   }
 }
 
-template <class G>
+template <class G, int POL>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
     int H, int W, int ngrp, int ntx, float inv_divisor, OutEpi epi) {
@@ -310,7 +324,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
     const RowRsrc rr{img2, img_bytes, (uint32_t)W * 4u, Y0, py, H};
 #endif
     loader_from<G, 0>(rr, rel, lds0);
-    CENSUS_FLUSH(8, 10);
+    CENSUS_FLUSH(13, 16, 0);
     return;
   }
 
@@ -333,9 +347,14 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
   // steps whose output row (2 (Y0 + 2 st + qd) + py) lies inside the image
   lc.nstep_ok = yrow0 < H ? min(G::NSTEP, (H - 1 - yrow0) / (2 * G::NQD) + 1) : 0;
 
+  // POL 1 (measurement): nt stores, step 0's f1 loads issued after the first DMA group landed
+  constexpr bool F1LATE = POL == 1;
+  constexpr int SPOL = POL == 1 ? 2 : POL;
   f32x4 f1[G::CH];
+  if constexpr (!F1LATE) {
 #pragma unroll
-  for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, 0, k);
+    for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, 0, k);
+  }
 
   // output: one buffer resource over the image's 81 planes; a store whose lane has nothing to
   // write (idle task, row or strip outside the image, the high half's fifth store) gets an
@@ -357,22 +376,28 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
       for (int e = 0; e < 4; ++e) acc[a][e] = 0.f;
     f32x4 wA[5], wB[5];
     __builtin_amdgcn_s_barrier();  // step 0: group 0 landed; later steps: their rows landed
+    if constexpr (F1LATE && ST == 0) {
+#pragma unroll
+      for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, 0, k);
+    }
     if (ST == 0) STAMP(1);
     read5<ST * G::NQD * G::SIGMA * 16>(lc.addr, wA);
     channel<G, ST, 0>(lc, acc, f1, wA, wB);
-    STAMP(2 + 2 * ST);  // loop done
+    STAMP(2 + 3 * ST);  // loop done
     // channel halves: lane l (c < C/2) and l + 32 (c >= C/2) hold partial sums of the same
     // task.  One v_permlane32_swap per pair (ti, ti + 5) leaves both halves of the pair in
     // each lane; their sum is displacement ti's total in one half and ti + 5's in the other.
     float res[5][4];
 #pragma unroll
-    for (int ti = 0; ti < 5; ++ti)
+    for (int ti = 0; ti < 5; ++ti) {
+      float a[4], b[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a = acc[ti][e], b = ti < 4 ? acc[ti + 5][e] : acc[ti][e];
-        swap32(a, b);
-        res[ti][e] = a + b;
-      }
+      for (int e = 0; e < 4; ++e) a[e] = acc[ti][e], b[e] = ti < 4 ? acc[ti + 5][e] : acc[ti][e];
+      swap32x4(a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) res[ti][e] = a[e] + b[e];
+    }
+    STAMP(3 + 3 * ST);  // channel halves reduced
     const int yrow = yrow0 + 2 * G::NQD * ST;
     const bool wr = active && px < W && ST < lc.nstep_ok;
     // the swap pairs (ti, ti + 5): the low half keeps ti, the high half ti + 5
@@ -389,15 +414,16 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
       }
       const bool ok = wr && (q < 4 || chalf == 0);
       __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0,
-                                             2 /* nt */);
+                                             SPOL);
     }
-    STAMP(3 + 2 * ST);  // stores issued
+    STAMP(4 + 3 * ST);  // stores issued
   };
   step(std::integral_constant<int, 0>{});
   if constexpr (G::NSTEP > 1) step(std::integral_constant<int, 1>{});
   if constexpr (G::NSTEP > 2) step(std::integral_constant<int, 2>{});
   static_assert(G::NSTEP <= 3, "unrolled steps");
-  if (wave == 0) CENSUS_FLUSH(0, 8);
+  if (wave == 0) CENSUS_FLUSH(0, 11, 0);
+  if (wave == G::WPP) CENSUS_FLUSH(0, 11, 16);  // the second quad's first wave
 }
 
 template <class G>
@@ -411,10 +437,15 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_strip<G>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-    if (e != hipSuccess) return e;
+    for (const void* f : {reinterpret_cast<const void*>(&corr_fwd_strip<G, 2>),
+                          reinterpret_cast<const void*>(&corr_fwd_strip<G, 16>),
+                          reinterpret_cast<const void*>(&corr_fwd_strip<G, 18>),
+                          reinterpret_cast<const void*>(&corr_fwd_strip<G, 0>),
+                          reinterpret_cast<const void*>(&corr_fwd_strip<G, 1>)}) {
+      const hipError_t e =
+          hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
   int ex;
@@ -425,9 +456,24 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   if (!(epi.slope <= 1.f)) return hipErrorNotSupported;  // max(v, slope v) form
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
-  hipExtLaunchKernelGGL((corr_fwd_strip<G>), dim3((unsigned)nblk), dim3(G::THREADS),
-                        G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,
-                        (float*)out, H, W, ngrp, ntx, inv, epi);
+  // output cache policy (buffer store aux bits): 2 nt, 16 sc1 (write-through), 18 nt sc1,
+  // 0 plain -- knob strip_st (measurement)
+  const int pol = debug_knob("strip_st", 2);
+#define PWC_STRIP_LAUNCH(P)                                                                     \
+  hipExtLaunchKernelGGL((corr_fwd_strip<G, P>), dim3((unsigned)nblk), dim3(G::THREADS),         \
+                        G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1,                   \
+                        (const float*)in2, (float*)out, H, W, ngrp, ntx, inv, epi)
+  if (pol == 16)
+    PWC_STRIP_LAUNCH(16);
+  else if (pol == 18)
+    PWC_STRIP_LAUNCH(18);
+  else if (pol == 0)
+    PWC_STRIP_LAUNCH(0);
+  else if (pol == 1)
+    PWC_STRIP_LAUNCH(1);
+  else
+    PWC_STRIP_LAUNCH(2);
+#undef PWC_STRIP_LAUNCH
   return hipGetLastError();
 }
 

@@ -211,46 +211,53 @@ int main(int argc, char** argv) {
   std::sort(vb.begin(), vb.end());
 #ifdef PWC_STRIP_CENSUS
   {
-    // one more batch of launches with the census buffer armed: per launch, the time of each
-    // stamp's LATEST workgroup relative to the launch's earliest workgroup start, averaged
+    // one more batch of launches with the census buffer armed: per launch, each stamp's
+    // LATEST workgroup relative to the launch's earliest workgroup start, and the mean
+    // per-workgroup span from its own start (us); quad A = wave 0, quad B = wave 4
     const int nb = B * 2 * (((H + 1) / 2 + 5) / 6) * (W / 56), CI = 50;
     unsigned long long* cen;
-    CK(hipMalloc(&cen, (size_t)CI * nb * 16 * 8));
-    CK(hipMemset(cen, 0, (size_t)CI * nb * 16 * 8));
+    CK(hipMalloc(&cen, (size_t)CI * nb * 32 * 8));
+    CK(hipMemset(cen, 0, (size_t)CI * nb * 32 * 8));
     for (int i = 0; i < CI; ++i) {
-      unsigned long long* p = cen + (size_t)i * nb * 16;
+      unsigned long long* p = cen + (size_t)i * nb * 32;
       CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::strip::g_census), &p, sizeof(p)));
       CK(pwc::corr_forward_strip(f1[i % NS], f2[i % NS], o2[i % NS], B, C, H, W, 32.f, 0));
     }
+    unsigned long long* np = nullptr;
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::strip::g_census), &np, sizeof(np)));
     CK(hipDeviceSynchronize());
-    std::vector<unsigned long long> c((size_t)CI * nb * 16);
+    std::vector<unsigned long long> c((size_t)CI * nb * 32);
     CK(hipMemcpy(c.data(), cen, c.size() * 8, hipMemcpyDeviceToHost));
-    double mx[16] = {}, mean[16] = {}, skew = 0;
+    double mx[32] = {}, mean[32] = {}, skew = 0;
     for (int i = 0; i < CI; ++i) {
-      const unsigned long long* L = c.data() + (size_t)i * nb * 16;
+      const unsigned long long* L = c.data() + (size_t)i * nb * 32;
       unsigned long long t0 = ~0ull, t0max = 0;
       for (int b = 0; b < nb; ++b) {
-        t0 = std::min(t0, L[b * 16]);
-        t0max = std::max(t0max, L[b * 16]);
+        t0 = std::min(t0, L[b * 32]);
+        t0max = std::max(t0max, L[b * 32]);
       }
       skew += (t0max - t0) * 0.01;
-      for (int k = 1; k < 10; ++k) {
+      for (int k = 1; k < 32; ++k) {
         unsigned long long m = 0;
         double sm = 0;
         for (int b = 0; b < nb; ++b) {
-          m = std::max(m, L[b * 16 + k]);
-          sm += (double)(L[b * 16 + k] - L[b * 16]);
+          m = std::max(m, L[b * 32 + k]);
+          sm += L[b * 32 + k] ? (double)(L[b * 32 + k] - L[b * 32]) : 0.0;
         }
-        mx[k] += (m - t0) * 0.01;
+        mx[k] += m ? (m - t0) * 0.01 : 0.0;
         mean[k] += sm / nb * 0.01;
       }
     }
-    const char* nm[10] = {"start", "first_data", "s0_loop", "s0_stored", "s1_loop", "s1_stored",
-                          "s2_loop", "s2_stored", "window_landed", "all_landed"};
+    const char* nm[16] = {"start", "first_data", "s0_loop", "s0_reduced", "s0_stored",
+                          "s1_loop", "s1_reduced", "s1_stored", "s2_loop", "s2_reduced",
+                          "s2_stored", "", "", "ld_group0", "ld_window", "ld_all"};
     std::printf("{\"census_start_skew_us\": %.2f", skew / CI);
-    for (int k = 1; k < 10; ++k)
-      std::printf(", \"%s\": [%.2f, %.2f]", nm[k], mx[k] / CI, mean[k] / CI);
-    std::printf("}  (latest workgroup vs earliest start, mean per-workgroup span; us)\n");
+    for (int k = 1; k < 16; ++k)
+      if (nm[k][0]) std::printf(", \"%s\": [%.2f, %.2f]", nm[k], mx[k] / CI, mean[k] / CI);
+    std::printf(", \"quadB\": {");
+    for (int k = 17; k < 27; ++k)
+      std::printf("%s\"%s\": %.2f", k > 17 ? ", " : "", nm[k - 16], mean[k] / CI);
+    std::printf("}}  ([latest workgroup vs earliest start, mean per-workgroup span] us)\n");
   }
 #endif
   const double bytes = (double)B * (2.0 * C * H * W + 81.0 * H * W) * 4;
