@@ -283,7 +283,7 @@ __device__ __forceinline__ void channel(const LaneCtx& lc, float (&acc)[9][4], f
   }
 }
 
-template <class G, int POL>
+template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
     int H, int W, int ngrp, int ntx, float inv_divisor, OutEpi epi) {
@@ -347,14 +347,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
   // steps whose output row (2 (Y0 + 2 st + qd) + py) lies inside the image
   lc.nstep_ok = yrow0 < H ? min(G::NSTEP, (H - 1 - yrow0) / (2 * G::NQD) + 1) : 0;
 
-  // POL 1 (measurement): nt stores, step 0's f1 loads issued after the first DMA group landed
-  constexpr bool F1LATE = POL == 1;
-  constexpr int SPOL = POL == 1 ? 2 : POL;
   f32x4 f1[G::CH];
-  if constexpr (!F1LATE) {
 #pragma unroll
-    for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, 0, k);
-  }
+  for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, 0, k);
 
   // output: one buffer resource over the image's 81 planes; a store whose lane has nothing to
   // write (idle task, row or strip outside the image, the high half's fifth store) gets an
@@ -376,10 +371,6 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
       for (int e = 0; e < 4; ++e) acc[a][e] = 0.f;
     f32x4 wA[5], wB[5];
     __builtin_amdgcn_s_barrier();  // step 0: group 0 landed; later steps: their rows landed
-    if constexpr (F1LATE && ST == 0) {
-#pragma unroll
-      for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, 0, k);
-    }
     if (ST == 0) STAMP(1);
     read5<ST * G::NQD * G::SIGMA * 16>(lc.addr, wA);
     channel<G, ST, 0>(lc, acc, f1, wA, wB);
@@ -413,8 +404,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
         v[e] = __builtin_bit_cast(uint32_t, fmaxf(o, o * slope));
       }
       const bool ok = wr && (q < 4 || chalf == 0);
-      __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0,
-                                             SPOL);
+      // nontemporal (aux 2): measured against sc1, nt sc1 and plain stores, 14.2 against
+      // 17.0-19.9 us back to back (profiles/r04a_strip_store_policy.txt)
+      __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0, 2);
     }
     STAMP(4 + 3 * ST);  // stores issued
   };
@@ -437,15 +429,10 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void* f : {reinterpret_cast<const void*>(&corr_fwd_strip<G, 2>),
-                          reinterpret_cast<const void*>(&corr_fwd_strip<G, 16>),
-                          reinterpret_cast<const void*>(&corr_fwd_strip<G, 18>),
-                          reinterpret_cast<const void*>(&corr_fwd_strip<G, 0>),
-                          reinterpret_cast<const void*>(&corr_fwd_strip<G, 1>)}) {
-      const hipError_t e =
-          hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-      if (e != hipSuccess) return e;
-    }
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_strip<G>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             G::LDS_BYTES);
+    if (e != hipSuccess) return e;
     attr_set = true;
   }
   int ex;
@@ -456,24 +443,9 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   if (!(epi.slope <= 1.f)) return hipErrorNotSupported;  // max(v, slope v) form
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
-  // output cache policy (buffer store aux bits): 2 nt, 16 sc1 (write-through), 18 nt sc1,
-  // 0 plain -- knob strip_st (measurement)
-  const int pol = debug_knob("strip_st", 2);
-#define PWC_STRIP_LAUNCH(P)                                                                     \
-  hipExtLaunchKernelGGL((corr_fwd_strip<G, P>), dim3((unsigned)nblk), dim3(G::THREADS),         \
-                        G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1,                   \
-                        (const float*)in2, (float*)out, H, W, ngrp, ntx, inv, epi)
-  if (pol == 16)
-    PWC_STRIP_LAUNCH(16);
-  else if (pol == 18)
-    PWC_STRIP_LAUNCH(18);
-  else if (pol == 0)
-    PWC_STRIP_LAUNCH(0);
-  else if (pol == 1)
-    PWC_STRIP_LAUNCH(1);
-  else
-    PWC_STRIP_LAUNCH(2);
-#undef PWC_STRIP_LAUNCH
+  hipExtLaunchKernelGGL((corr_fwd_strip<G>), dim3((unsigned)nblk), dim3(G::THREADS),
+                        G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,
+                        (float*)out, H, W, ngrp, ntx, inv, epi);
   return hipGetLastError();
 }
 

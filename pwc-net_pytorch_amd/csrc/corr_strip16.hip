@@ -10,15 +10,16 @@
 // The strip design of corr_strip.hip carried to many rows: a workgroup owns a
 // 128-px column strip of 14 parity rows and produces them two per STEP (7 steps), with the f2
 // rows of the step window in an LDS ring (row m in slot m % 12): while step s computes rows
-// 2s, 2s+1 from f2 rows 2s .. 2s+9, a loader wave stages f2 rows 2s+10, 2s+11 (into the slots
+// 2s, 2s+1 from f2 rows 2s .. 2s+9, two loader waves stage f2 rows 2s+10, 2s+11 (into the slots
 // step s-1 freed) and the next step's f1 rows, and step s's stores drain under step s+1.  One
 // workgroup per CU for the whole launch: the window slides instead of being reloaded, and the
 // start-up and the store tail are paid once, not once per round.
 //
 //   * LDS holds channel PAIRS: pixel x of channels (c, c+1) as one half2 dword.  The loader
 //     packs them from two 16-B global loads (8 pixels of channel c and of c + 1) with v_perm --
-//     per step 2 f2 rows + 2 f1 rows, ~17 items per loader lane: the loader is not the bound
-//     here, unlike the band-restaging stream kernel's (profiles/r03f_cfg4_mfma_bound.txt).
+//     per step 2 f2 rows + 2 f1 rows = 544 items, <= 5 per loader lane, all loads of a step in
+//     flight before the first pack (one memory latency per step; with one loader wave in batches
+//     of 3 the step paid three and the launch took 60 % longer).
 //   * compute lane = (row of the step, tj, 4-px segment), all 16 channel pairs: per pair 5
 //     ds_read_b128 of the f2 window + 1 of f1, 36 v_dot2_f32_f16 into 4 px x 9 ti fp32 sums.
 //     2 rows x 9 tj x 32 segments = 576 tasks = 9 waves exactly.  A wave's lanes 0-31 (and
@@ -59,7 +60,8 @@ struct Geo {
   static constexpr int WIN = NQD + 8;       // f2 rows of one step
   static constexpr int NTASK = NQD * 9 * NSEG;
   static constexpr int NWC = NTASK / 64;    // compute waves
-  static constexpr int THREADS = 64 * (NWC + 1);
+  static constexpr int NWL = 2;             // loader waves
+  static constexpr int THREADS = 64 * (NWC + NWL);
   static constexpr int F2_B = NSL * ROWQ * 16;
   static constexpr int F1_B = 2 * NQD * F1ROWQ * 16;  // double-buffered by step parity
   static constexpr int LDS_BYTES = F2_B + F1_B;
@@ -224,10 +226,21 @@ __device__ __forceinline__ void stage_rows(float* lds, const Ctx& c, int tid, in
   }
 }
 
+// loader items per lane per step (2 f2 rows + 2 f1 rows over the loader waves): one batch
+constexpr int kLoaderB = (Geo::NQD * (Geo::UF2 + Geo::UF1) + 64 * Geo::NWL - 1) / (64 * Geo::NWL);
+
+#ifdef PWC_CENSUS
+// measurement build only (make CENSUS=1): ablation mask from knob s16_abl -- 1: no LDS reads /
+// dot products, 2: no stores, 4: loader stages nothing after the first barrier
+#define S16_ABL(bit) (abl & (bit))
+#else
+#define S16_ABL(bit) 0
+#endif
+
 template <int POL>
 __global__ __launch_bounds__(Geo::THREADS, 1) void corr_fwd_strip16(
     const __half* __restrict__ in1, const __half* __restrict__ in2, __half* __restrict__ out,
-    int H, int W, int nchunk, int ntx, float inv_divisor, OutEpi epi) {
+    int H, int W, int nchunk, int ntx, float inv_divisor, OutEpi epi, int abl) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // logical block = (n, row parity, chunk, strip), strip fastest (XCD neighbours share rows)
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -246,22 +259,28 @@ __global__ __launch_bounds__(Geo::THREADS, 1) void corr_fwd_strip16(
   c.rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)img2, (short)0, (int)img_bytes, 0x00020000);
   c.H = H, c.W = W, c.Y0 = ch * Geo::RCH, c.py = py, c.x0 = tx * Geo::TW;
 
-  // every wave stages step 0's window (f2 rows 0..9) and f1 rows; the loader wave then stages
+  // every wave stages step 0's window (f2 rows 0..9) and f1 rows; the loader waves then stage
   // rows 10, 11 before the first barrier
   stage_rows<3>(lds, c, threadIdx.x, Geo::THREADS, 0, 0, Geo::WIN, true);
-  if (wave == Geo::NWC) {
-    // ---------------- loader wave ----------------
-    stage_rows<3>(lds, c, lane, 64, 0, Geo::WIN, Geo::WIN + Geo::NQD, false);
+  if (wave >= Geo::NWC) {
+    const int ltid = threadIdx.x - 64 * Geo::NWC;
+    // ---------------- loader waves ----------------
+    stage_rows<kLoaderB>(lds, c, ltid, 64 * Geo::NWL, 0, Geo::WIN, Geo::WIN + Geo::NQD, false);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // B_0
     // Between B_s and B_{s+1} (step s computing): the f1 rows of step s+1 (buffer (s+1) & 1,
     // last read by step s-1) and, from s = 1 on, the two f2 rows step s+1 adds (rows 2s+10,
     // 2s+11 into the slots of rows 2s-2, 2s-1, last read by step s-1); step 1's (rows 10, 11)
     // were staged before B_0.
+    // One batch per step (every item's loads in flight before the first pack): the loader pays
+    // one memory latency per step, not one per 3 items.
     for (int s = 0; s + 1 < Geo::NSTEP; ++s) {
       const int m0 = Geo::WIN + Geo::NQD * s;
-      if (s > 0 && m0 < Geo::NROW) stage_rows<3>(lds, c, lane, 64, 0, m0, m0 + Geo::NQD, false);
-      stage_rows<3>(lds, c, lane, 64, s + 1, 0, 0, true);  // f1 rows of step s+1
+      if (S16_ABL(4)) {
+      } else if (s > 0 && m0 < Geo::NROW)
+        stage_rows<kLoaderB>(lds, c, ltid, 64 * Geo::NWL, s + 1, m0, m0 + Geo::NQD, true);
+      else
+        stage_rows<kLoaderB>(lds, c, ltid, 64 * Geo::NWL, s + 1, 0, 0, true);  // f1 rows of step s+1
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B_{s+1}: step s done, step s+1's rows landed
     }
@@ -291,12 +310,14 @@ __global__ __launch_bounds__(Geo::THREADS, 1) void corr_fwd_strip16(
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[q][e] = 0.f;
     f32x4 wA[5], wB[5], xA, xB;
-    read6<0, 0>(a, f, wA, xA);
-    pair_loop<0>(a, f, acc, wA, xA, wB, xB);
+    if (!S16_ABL(1)) {
+      read6<0, 0>(a, f, wA, xA);
+      pair_loop<0>(a, f, acc, wA, xA, wB, xB);
+    }
     // epilogue: 9 stores of 4 px (8 B) per lane; a lane with nothing to write (row or strip
     // outside the image) gets an out-of-range offset (branch-free stores)
     const int y = 2 * (c.Y0 + Geo::NQD * s + r) + py;
-    const bool ok = y < H && px < W;
+    const bool ok = y < H && px < W && !S16_ABL(2);
     const uint32_t o0 = (uint32_t)(((tj * 9) * H + y) * W + px) * 2u;
 #pragma unroll
     for (int ti = 0; ti < 9; ++ti) {
@@ -357,11 +378,16 @@ hipError_t corr_forward_strip16(const void* in1, const void* in2, void* out, int
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+#ifdef PWC_CENSUS
+  const int abl = debug_knob("s16_abl", 0);
+#else
+  const int abl = 0;
+#endif
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
   hipExtLaunchKernelGGL((strip16::corr_fwd_strip16<2>), dim3((unsigned)nblk), dim3(G::THREADS),
                         G::LDS_BYTES, stream, ev0, ev1, 0, (const __half*)in1,
-                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, epi);
+                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, epi, abl);
   return hipGetLastError();
 }
 

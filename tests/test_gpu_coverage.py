@@ -72,6 +72,12 @@ FWD = [
     ("corr9", torch.float32, (6, 32, 96, 112), "strip, B=6"),
     ("corr9", torch.float32, (8, 32, 90, 112), "strip, partial row group"),
     ("corr9", torch.float32, (4, 32, 192, 224), "strip, 4 strips per row"),
+    # the matrix-core fp16 strip kernel (corr_mstrip16.hip): its smallest batch at Sintel l4, a
+    # partial last chunk (50 parity rows in chunks of 14) with a partial last strip (W = 200),
+    # and an odd height (parity rows 50 / 49)
+    ("corr9", torch.float16, (12, 32, 112, 256), "mstrip16, B=12"),
+    ("corr9", torch.float16, (16, 32, 100, 200), "mstrip16, partial chunk and strip"),
+    ("corr9", torch.float16, (24, 32, 99, 128), "mstrip16, odd height"),
 ]
 
 
@@ -111,6 +117,22 @@ def test_strip_into_cat_slice_leaky():
     ref = O.corr_forward(an, bn, 9, 1, 9, 1, 2)
     ref = np.where(ref > 0, ref, ref * 0.01)
     np.testing.assert_allclose(_np(cat[:, C:C + 81]), ref, rtol=1e-5, atol=1e-5)
+    assert bool((cat[:, :C] == 7.0).all()) and bool((cat[:, C + 81:] == 7.0).all())
+
+
+def test_mstrip16_into_cat_slice_leaky():
+    """model.py:83-84 + :89/91 at config 4's l4 (fp16) through the matrix-core strip kernel: the
+    volume written into the cat buffer's slice with leaky_relu(0.1) fused, the rest untouched."""
+    from pwcnet_amd.ops import corr_forward_into
+    B, C, H, W = 12, 32, 112, 256
+    a, an = _rand((B, C, H, W), torch.float16, "ma")
+    b, bn = _rand((B, C, H, W), torch.float16, "mb")
+    cat = torch.full((B, C + 81 + 2, H, W), 7.0, device=DEV, dtype=torch.float16)
+    corr_forward_into(a, b, cat[:, C:C + 81], 9, 1, 9, 1, 2, negative_slope=0.1)
+    torch.cuda.synchronize()
+    ref = O.corr_forward(an, bn, 9, 1, 9, 1, 2)
+    ref = np.where(ref > 0, ref, ref * 0.1)
+    _check(cat[:, C:C + 81], ref, torch.float16)
     assert bool((cat[:, :C] == 7.0).all()) and bool((cat[:, C + 81:] == 7.0).all())
 
 

@@ -18,6 +18,8 @@
 
 #include "../pwc-net_pytorch_amd/csrc/corr_stream.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_strip.hip"
+#include "../pwc-net_pytorch_amd/csrc/corr_strip16.hip"
+#include "../pwc-net_pytorch_amd/csrc/corr_mstrip16.hip"
 
 namespace pwc {
 hipEvent_t g_e0 = nullptr, g_e1 = nullptr;
