@@ -337,7 +337,7 @@ bool corr_mstrip16_accepts(const void* in1, const void* in2, const void* out, in
   if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16) return false;
   if (W % 8 || W < 64 || H < 2 || (size_t)C * H * W * 2 >= 0x7ffffff0ull) return false;
   if ((size_t)81 * H * W * 2 >= 0x7ffffff0ull) return false;
-  if (debug_knob("mstrip16", 0) == 0) return false;  // off until verified on the GPU
+  if (debug_knob("mstrip16", 1) == 0) return false;
   const long long nblk = (long long)B * 2 * (((H + 1) / 2 + G::RCH - 1) / G::RCH) *
                          ((W + G::TW - 1) / G::TW);
   return nblk >= 192;

@@ -762,10 +762,6 @@ bool corr_stream_accepts(const void* in1, const void* in2, const void* out, int 
 }
 
 bool corr_strip_accepts(const void*, const void*, const void*, int, int, int, int, int, int, int);
-bool corr_strip16_accepts(const void*, const void*, const void*, int, int, int, int, int, int,
-                          int);
-hipError_t corr_forward_strip16(const void*, const void*, void*, int, int, int, int, float,
-                                hipStream_t);
 hipError_t corr_forward_strip(const void*, const void*, void*, int, int, int, int, float,
                               hipStream_t);
 bool corr_mstrip16_accepts(const void*, const void*, const void*, int, int, int, int, int, int,
@@ -783,14 +779,9 @@ hipError_t corr_forward_stream(const void* in1, const void* in2, void* out, int 
     const hipError_t e = corr_forward_strip(in1, in2, out, B, C, H, W, divisor, stream);
     if (e != hipErrorNotSupported) return e;
   }
-  // fp16 storage, C = 32 (config-4 l4): the matrix-core strip kernel (corr_mstrip16.hip), then
-  // the VALU sliding-window one (corr_strip16.hip)
+  // fp16 storage, C = 32 (config-4 l4): the matrix-core strip kernel (corr_mstrip16.hip)
   if (corr_mstrip16_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)) {
     const hipError_t e = corr_forward_mstrip16(in1, in2, out, B, C, H, W, divisor, stream);
-    if (e != hipErrorNotSupported) return e;
-  }
-  if (corr_strip16_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)) {
-    const hipError_t e = corr_forward_strip16(in1, in2, out, B, C, H, W, divisor, stream);
     if (e != hipErrorNotSupported) return e;
   }
   const int twp = (W % 112 == 0 || W < 112) ? 112 : 128;  // column tile width in pixels

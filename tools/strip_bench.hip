@@ -18,7 +18,6 @@
 
 #include "../pwc-net_pytorch_amd/csrc/corr_stream.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_strip.hip"
-#include "../pwc-net_pytorch_amd/csrc/corr_strip16.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_mstrip16.hip"
 
 namespace pwc {
