@@ -57,27 +57,44 @@ typedef short s16x4v __attribute__((__vector_size__(4 * sizeof(short))));
 typedef __attribute__((address_space(3))) s16x4v lds_s16x4;
 typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
 
+// halves per staged (parity, channel) row: >= NU + 8 (the f2 halo), and RS/2 dwords = 8 (mod 16)
+// so the eight channel rows one 32-lane half of a transposed read takes sit on distinct 8-dword
+// bank groups
+constexpr int row_halves(int nu) { return 2 * (16 * ((nu + 8 - 8 + 31) / 32) + 8); }
+
+// C channels, TW-px strips, RCH parity rows (steps) per workgroup.  Config-4 l4: <32, 128, 14>
+// (four 16-u blocks, one compute wave each); config-4 l3: <64, 64, 7> (two 16-u blocks, the 9
+// displacement rows split 5 + 4 over two waves each; K = 64 as two MFMAs per block).
+template <int C_, int TW_, int RCH_>
 struct Geo {
-  static constexpr int C = 32;
-  static constexpr int TW = 128;            // strip width (px)
-  static constexpr int NU = TW / 2;         // pixels per parity
-  static constexpr int RS = 80;             // halves per (parity, channel) row; f2 uses 72
-  static constexpr int EB = C * RS * 2;     // bytes per parity plane of a staged row
-  static constexpr int ROWB = 2 * EB;       // bytes per staged row
-  static constexpr int RCH = 14;            // parity rows per workgroup = steps
-  static constexpr int NSL = 11;            // f2 ring: a step's 9 rows + the 2 staged ahead
+  static constexpr int C = C_, TW = TW_, RCH = RCH_;
+  static constexpr int KC = C / 32;                // MFMA K chunks
+  static constexpr int NU = TW / 2;                // pixels per parity
+  static constexpr int NUB = NU / 16;              // 16-u blocks
+  static constexpr int TS = 4 / NUB;               // displacement-row splits per block
+  static constexpr int RS = row_halves(NU);
+  static constexpr int EB = C * RS * 2;            // bytes per parity plane of a staged row
+  static constexpr int ROWB = 2 * EB;              // bytes per staged row
+  static constexpr int NSL = 11;                   // f2 ring: a step's 9 rows + 2 staged ahead
   static constexpr int LDS_BYTES = (NSL + 2) * ROWB;
-  static constexpr int NWC = 4;             // compute waves: one 16-u block each
-  static constexpr int NWL = 4;             // loader waves
+  static constexpr int NWC = NUB * TS;             // compute waves
+  static constexpr int NWL = 4;                    // loader waves
   static constexpr int THREADS = 64 * (NWC + NWL);
-  static constexpr int IF2 = C * (TW + 16) / 8;  // 16-B load items per f2 row (8-px halo each side)
-  static constexpr int IF1 = C * TW / 8;         // per f1 row
-  static constexpr int LT = 64 * NWL;            // loader lanes
-  static constexpr int LB = (IF2 + IF1 + LT - 1) / LT;  // items per loader lane per step
-  static_assert(NU == 16 * NWC, "one 16-u block per compute wave");
+  static constexpr int G2 = TW / 8 + 2;            // 8-px groups per f2 row (8-px halo each side)
+  static constexpr int G1 = TW / 8;                // ... per f1 row
+  static constexpr int IF2 = C * G2;               // 16-B load items per f2 row
+  static constexpr int IF1 = C * G1;               // per f1 row
+  static constexpr int LT = 64 * NWL;              // loader lanes
+  static constexpr int NK2 = (IF2 + LT - 1) / LT;  // loader slots: f2 row, then f1 row
+  static constexpr int NK1 = IF1 / LT;
+  static constexpr int LB = NK2 + NK1;
+  static_assert(NWC == 4 && NUB * 16 == NU && C % 32 == 0, "four compute waves, 16-u blocks");
   static_assert((RS / 2) % 16 == 8 && RS >= NU + 8, "8 channel rows on distinct bank groups");
+  static_assert(NK1 * LT == IF1, "f1 items fill the loader slots");
   static_assert(LDS_BYTES <= 160 * 1024 && THREADS <= 1024, "workgroup resources");
 };
+using GeoL4 = Geo<32, 128, 14>;
+using GeoL3 = Geo<64, 64, 7>;
 
 constexpr uint32_t kOOB = 0x80000000u;
 
@@ -88,30 +105,28 @@ struct Ctx {
 };
 
 // A loader lane's items of one step: NK2 slots of the new f2 row (item i = lane + LT k, channel
-// i / 18, 8-px group i % 18: 18 consecutive lanes read 288 contiguous bytes of one channel row),
-// then NK1 slots of the f1 row (channel i / 16).  Per lane the global offset without the row
-// term and the LDS offset without the buffer base are fixed; each step adds uniform row terms, so
-// a load instruction is all-f2 or all-f1 (a uniform buffer resource).
-constexpr int NK2 = (Geo::IF2 + Geo::LT - 1) / Geo::LT;
-constexpr int NK1 = Geo::IF1 / Geo::LT;
-static_assert(NK1 * Geo::LT == Geo::IF1 && NK2 + NK1 == Geo::LB, "loader slots");
-
+// i / G2, 8-px group i % G2: consecutive lanes read contiguous bytes of one channel row), then
+// NK1 slots of the f1 row.  Per lane the global offset without the row term and the LDS offset
+// without the buffer base are fixed; each step adds uniform row terms, so a load instruction is
+// all-f2 or all-f1 (a uniform buffer resource).
+template <class G>
 struct LaneItems {
-  uint32_t g[Geo::LB];  // global byte offset of the item's 8 px in row 0, or kOOB
-  int l[Geo::LB];       // LDS byte of its even run within a staged row, -1: no item
+  uint32_t g[G::LB];  // global byte offset of the item's 8 px in row 0, or kOOB
+  int l[G::LB];       // LDS byte of its even run within a staged row, -1: no item
 };
 
-__device__ __forceinline__ void lane_items(const Ctx& c, int lt, LaneItems& it) {
+template <class G>
+__device__ __forceinline__ void lane_items(const Ctx& c, int lt, LaneItems<G>& it) {
 #pragma unroll
-  for (int k = 0; k < Geo::LB; ++k) {
-    const bool f2 = k < NK2;
-    const int i = lt + Geo::LT * (f2 ? k : k - NK2);
-    const int per = f2 ? Geo::TW / 8 + 2 : Geo::TW / 8;
+  for (int k = 0; k < G::LB; ++k) {
+    const bool f2 = k < G::NK2;
+    const int i = lt + G::LT * (f2 ? k : k - G::NK2);
+    const int per = f2 ? G::G2 : G::G1;
     const int ch = i / per, kk = i % per;
     const int x = f2 ? c.x0 - 8 + 8 * kk : c.x0 + 8 * kk;
-    const bool have = f2 ? i < Geo::IF2 : true;
+    const bool have = f2 ? i < G::IF2 : true;
     it.g[k] = have && x >= 0 && x < c.W ? (uint32_t)ch * c.plane_b + (uint32_t)x * 2u : kOOB;
-    it.l[k] = have ? (ch * Geo::RS + 4 * kk) * 2 : -1;
+    it.l[k] = have ? (ch * G::RS + 4 * kk) * 2 : -1;
   }
 }
 
@@ -127,6 +142,7 @@ __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t rs, uint32_t g, u
 }
 
 // 8 pixels of one channel -> the 4 even and the 4 odd halves, one 8-B run in each parity plane
+template <class G>
 __device__ __forceinline__ void item_store(char* lds, int lds_b, const u32x4& d) {
   if (lds_b < 0) return;
   const u32x2 ev = {__builtin_amdgcn_perm(d.y, d.x, 0x05040100u),
@@ -134,32 +150,35 @@ __device__ __forceinline__ void item_store(char* lds, int lds_b, const u32x4& d)
   const u32x2 od = {__builtin_amdgcn_perm(d.y, d.x, 0x07060302u),
                     __builtin_amdgcn_perm(d.w, d.z, 0x07060302u)};
   *reinterpret_cast<u32x2*>(lds + lds_b) = ev;
-  *reinterpret_cast<u32x2*>(lds + lds_b + Geo::EB) = od;
+  *reinterpret_cast<u32x2*>(lds + lds_b + G::EB) = od;
 }
 
 // Step st's loads: f2 window row st + 8 and f1 row st
-__device__ __forceinline__ void step_issue(const Ctx& c, const LaneItems& it, int st,
-                                           u32x4 (&r)[Geo::LB]) {
+template <class G>
+__device__ __forceinline__ void step_issue(const Ctx& c, const LaneItems<G>& it, int st,
+                                           u32x4 (&r)[G::LB]) {
   const uint32_t r2 = row_off(c, c.Y0 - 4 + st + 8), r1 = row_off(c, c.Y0 + st);
 #pragma unroll
-  for (int k = 0; k < Geo::LB; ++k)
-    r[k] = k < NK2 ? load16(c.rs2, it.g[k], r2) : load16(c.rs1, it.g[k], r1);
+  for (int k = 0; k < G::LB; ++k)
+    r[k] = k < G::NK2 ? load16(c.rs2, it.g[k], r2) : load16(c.rs1, it.g[k], r1);
 }
 
-__device__ __forceinline__ void step_write(char* lds, const LaneItems& it, int st,
-                                           const u32x4 (&r)[Geo::LB]) {
-  const int b2 = ((st + 8) % Geo::NSL) * Geo::ROWB, b1 = (Geo::NSL + (st & 1)) * Geo::ROWB;
+template <class G>
+__device__ __forceinline__ void step_write(char* lds, const LaneItems<G>& it, int st,
+                                           const u32x4 (&r)[G::LB]) {
+  const int b2 = ((st + 8) % G::NSL) * G::ROWB, b1 = (G::NSL + (st & 1)) * G::ROWB;
 #pragma unroll
-  for (int k = 0; k < Geo::LB; ++k)
-    item_store(lds, it.l[k] < 0 ? -1 : it.l[k] + (k < NK2 ? b2 : b1), r[k]);
+  for (int k = 0; k < G::LB; ++k)
+    item_store<G>(lds, it.l[k] < 0 ? -1 : it.l[k] + (k < G::NK2 ? b2 : b1), r[k]);
 }
 
 // Both transposed reads of one 16 x 32 operand block: channels 4g + q, then 16 + 4g + q
+template <class G>
 __device__ __forceinline__ f16x8 tr_block(const char* lds, int byte) {
   typedef __attribute__((address_space(3))) char lchar;
   const lchar* p = (const lchar*)lds + byte;
   const s16x4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
-  const s16x4v b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 16 * Geo::RS * 2));
+  const s16x4v b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 16 * G::RS * 2));
   const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(f16x8, v);
 }
@@ -183,8 +202,71 @@ __device__ __forceinline__ f32x4 diag(const f32x4& d1, const f32x4& d2, bool lo_
   return __builtin_bit_cast(f32x4, r);
 }
 
-template <int POL>
-__global__ __launch_bounds__(Geo::THREADS, 1) void corr_fwd_mstrip16(
+// The operand blocks of one displacement row: [parity][u' block][K chunk]
+template <class G>
+struct BOps {
+  f16x8 v[2][2][G::KC];
+};
+
+template <class G>
+__device__ __forceinline__ void read_b(const char* lds, int f2b, BOps<G>& b) {
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < G::KC; ++k)
+        b.v[e][h][k] = tr_block<G>(lds, f2b + e * G::EB + 16 * h + k * 32 * G::RS * 2);
+}
+
+// Displacement rows TJ0 .. TJ0 + NTJ - 1 of one output row: the next row's operand blocks are
+// read while this row's products, diagonals and store run.
+template <class G, int TJ0, int NTJ>
+__device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
+                                        const f16x8 (&a)[2][G::KC], bool lo_half, bool plain,
+                                        float inv_divisor, float slope,
+                                        __amdgpu_buffer_rsrc_t rso, uint32_t o0, uint32_t pstep,
+                                        bool lane_ok, int jj) {
+  int sl = slot0 + TJ0;
+  sl = sl >= G::NSL ? sl - G::NSL : sl;
+  BOps<G> bc, bn;
+  read_b<G>(lds, sl * G::ROWB + lane_b, bc);
+#pragma unroll
+  for (int t = 0; t < NTJ; ++t) {
+    const int tj = TJ0 + t;
+    sl = sl + 1 == G::NSL ? 0 : sl + 1;
+    if (t + 1 < NTJ) read_b<G>(lds, sl * G::ROWB + lane_b, bn);
+    f32x4 e[2];
+#pragma unroll
+    for (int pe = 0; pe < 2; ++pe) {
+      f32x4 d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < G::KC; ++k) {
+        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[pe][k], bc.v[pe][0][k], d1, 0, 0, 0);
+        d2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[pe][k], bc.v[pe][1][k], d2, 0, 0, 0);
+      }
+      e[pe] = diag(d1, d2, lo_half) * inv_divisor;  // exact: 2^-k
+    }
+    u32x4 h;
+    if (plain) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        h[v] = __builtin_bit_cast(uint32_t, h2_t{(_Float16)e[0][v], (_Float16)e[1][v]});
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        h[v] = __builtin_bit_cast(uint32_t, h2_t{(_Float16)fmaxf(e[0][v], e[0][v] * slope),
+                                                 (_Float16)fmaxf(e[1][v], e[1][v] * slope)});
+    }
+    const uint32_t off = o0 + (uint32_t)(tj * 9 + jj) * pstep;
+    // nontemporal: the volume is read by the next layer, not by this kernel
+    __builtin_amdgcn_raw_buffer_store_b128(h, rso, (int)(lane_ok ? off : kOOB), 0, 2);
+    if (t + 1 < NTJ) bc = bn;
+  }
+}
+
+template <class G>
+__global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
     const __half* __restrict__ in1, const __half* __restrict__ in2, __half* __restrict__ out,
     int H, int W, int nchunk, int ntx, float inv_divisor, OutEpi epi) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -198,60 +280,62 @@ __global__ __launch_bounds__(Geo::THREADS, 1) void corr_fwd_mstrip16(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   Ctx c;
   c.plane_b = (uint32_t)(H * W) * 2u;
-  const uint32_t img_bytes = (uint32_t)Geo::C * c.plane_b;  // < 2^31 (launcher)
-  const __half* img1 = in1 + (size_t)n * Geo::C * H * W;
-  const __half* img2 = in2 + (size_t)n * Geo::C * H * W;
+  const uint32_t img_bytes = (uint32_t)G::C * c.plane_b;  // < 2^31 (launcher)
+  const __half* img1 = in1 + (size_t)n * G::C * H * W;
+  const __half* img2 = in2 + (size_t)n * G::C * H * W;
   c.rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)img1, (short)0, (int)img_bytes, 0x00020000);
   c.rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)img2, (short)0, (int)img_bytes, 0x00020000);
-  c.H = H, c.W = W, c.Y0 = ch * Geo::RCH, c.py = py, c.x0 = tx * Geo::TW;
+  c.H = H, c.W = W, c.Y0 = ch * G::RCH, c.py = py, c.x0 = tx * G::TW;
 
   // step 0's window (f2 rows 0..8) and f1 row: every wave, one batch (item i of the 9 x IF2
-  // window items: row i / IF2; then the f1 row over the first IF1 threads)
+  // window items: row i / IF2; then the f1 row)
   {
-    constexpr int SK = (9 * Geo::IF2 + Geo::THREADS - 1) / Geo::THREADS;
-    static_assert(Geo::IF1 <= Geo::THREADS, "one f1 slot");
-    u32x4 r[SK + 1];
-    int b[SK + 1];
+    constexpr int SK = (9 * G::IF2 + G::THREADS - 1) / G::THREADS;
+    constexpr int S1 = (G::IF1 + G::THREADS - 1) / G::THREADS;
+    u32x4 r[SK + S1];
+    int b[SK + S1];
 #pragma unroll
     for (int k = 0; k < SK; ++k) {
-      const int i = threadIdx.x + Geo::THREADS * k;
-      const int m = i / Geo::IF2, j = i % Geo::IF2;
-      const int ch = j / (Geo::TW / 8 + 2), kk = j % (Geo::TW / 8 + 2);
+      const int i = threadIdx.x + G::THREADS * k;
+      const int m = i / G::IF2, j = i % G::IF2;
+      const int chn = j / G::G2, kk = j % G::G2;
       const int x = c.x0 - 8 + 8 * kk;
       const bool have = m < 9;
-      r[k] = load16(c.rs2, have && x >= 0 && x < W ? (uint32_t)ch * c.plane_b + (uint32_t)x * 2u
-                                                   : kOOB,
+      r[k] = load16(c.rs2,
+                    have && x >= 0 && x < W ? (uint32_t)chn * c.plane_b + (uint32_t)x * 2u : kOOB,
                     row_off(c, c.Y0 - 4 + m));
-      b[k] = have ? m * Geo::ROWB + (ch * Geo::RS + 4 * kk) * 2 : -1;
-    }
-    {
-      const int i = threadIdx.x;
-      const int ch = i / (Geo::TW / 8), kk = i % (Geo::TW / 8);
-      const int x = c.x0 + 8 * kk;
-      const bool have = i < Geo::IF1;
-      r[SK] = load16(c.rs1, have && x < W ? (uint32_t)ch * c.plane_b + (uint32_t)x * 2u : kOOB,
-                     row_off(c, c.Y0));
-      b[SK] = have ? Geo::NSL * Geo::ROWB + (ch * Geo::RS + 4 * kk) * 2 : -1;
+      b[k] = have ? m * G::ROWB + (chn * G::RS + 4 * kk) * 2 : -1;
     }
 #pragma unroll
-    for (int k = 0; k <= SK; ++k) item_store(lds, b[k], r[k]);
+    for (int k = 0; k < S1; ++k) {
+      const int i = threadIdx.x + G::THREADS * k;
+      const int chn = i / G::G1, kk = i % G::G1;
+      const int x = c.x0 + 8 * kk;
+      const bool have = i < G::IF1;
+      r[SK + k] = load16(c.rs1,
+                         have && x < W ? (uint32_t)chn * c.plane_b + (uint32_t)x * 2u : kOOB,
+                         row_off(c, c.Y0));
+      b[SK + k] = have ? G::NSL * G::ROWB + (chn * G::RS + 4 * kk) * 2 : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < SK + S1; ++k) item_store<G>(lds, b[k], r[k]);
   }
 
-  if (wave >= Geo::NWC) {
+  if (wave >= G::NWC) {
     // ---------------- loader waves ----------------
-    LaneItems it;
-    lane_items(c, threadIdx.x - 64 * Geo::NWC, it);
-    u32x4 r[3][Geo::LB];
-    step_issue(c, it, 1, r[1]);
-    step_issue(c, it, 2, r[2]);
+    LaneItems<G> it;
+    lane_items<G>(c, threadIdx.x - 64 * G::NWC, it);
+    u32x4 r[3][G::LB];
+    if (G::RCH > 1) step_issue<G>(c, it, 1, r[1]);
+    if (G::RCH > 2) step_issue<G>(c, it, 2, r[2]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // B_0
 #pragma unroll
-    for (int s = 1; s < Geo::RCH; ++s) {
+    for (int s = 1; s < G::RCH; ++s) {
       // between B_{s-1} and B_s (step s-1 computing): step s+2's loads out, step s's rows in
       // (f2 row s+8 into the slot of row s-3, f1 into buffer s & 1, both last read by step s-2)
-      if (s + 2 < Geo::RCH) step_issue(c, it, s + 2, r[(s + 2) % 3]);
-      step_write(lds, it, s, r[s % 3]);
+      if (s + 2 < G::RCH) step_issue<G>(c, it, s + 2, r[(s + 2) % 3]);
+      step_write<G>(lds, it, s, r[s % 3]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B_s
     }
@@ -259,9 +343,10 @@ __global__ __launch_bounds__(Geo::THREADS, 1) void corr_fwd_mstrip16(
   }
 
   // ---------------- compute waves ----------------
-  const int ub = wave;  // 16-u block: pixels x0 + 32 ub .. + 31
+  const int ub = wave % G::NUB;  // 16-u block: pixels x0 + 32 ub .. + 31
+  const int th = wave / G::NUB;  // displacement-row split
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, jj = lane & 15;
-  const int lane_b = ((4 * g + q) * Geo::RS + 4 * p) * 2 + 32 * ub;
+  const int lane_b = ((4 * g + q) * G::RS + 4 * p) * 2 + 32 * ub;
   const bool lo_half = lane < 32;
   const int xs = c.x0 + 32 * ub + 8 * g;  // this lane's 8 output pixels
   const bool lane_ok = jj < 9 && xs < W;
@@ -272,80 +357,85 @@ __global__ __launch_bounds__(Geo::THREADS, 1) void corr_fwd_mstrip16(
   const bool plain = slope == 1.f;  // no fused leaky_relu
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's share of step 0's staging
   int slot0 = 0;                                       // slot of window row s
-  for (int s = 0; s < Geo::RCH; ++s) {
+  for (int s = 0; s < G::RCH; ++s) {
     __builtin_amdgcn_s_barrier();  // B_s: the step's rows are in LDS
     const int y = 2 * (c.Y0 + s) + py;
     if (y < H) {
-      const int f1b = (Geo::NSL + (s & 1)) * Geo::ROWB + lane_b;
-      const f16x8 a0 = tr_block(lds, f1b);
-      const f16x8 a1 = tr_block(lds, f1b + Geo::EB);
+      const int f1b = (G::NSL + (s & 1)) * G::ROWB + lane_b;
+      f16x8 a[2][G::KC];
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int k = 0; k < G::KC; ++k)
+          a[e][k] = tr_block<G>(lds, f1b + e * G::EB + k * 32 * G::RS * 2);
       const uint32_t o0 = ((uint32_t)y * W + xs) * 2u;
-      // software pipeline over tj: the next displacement row's four operand blocks are read
-      // while this row's products and diagonals run
-      int sl = slot0;
-      f16x8 bc[4], bn[4];
-      {
-        const int f2b = sl * Geo::ROWB + lane_b;
-        bc[0] = tr_block(lds, f2b), bc[1] = tr_block(lds, f2b + 16);
-        bc[2] = tr_block(lds, f2b + Geo::EB), bc[3] = tr_block(lds, f2b + Geo::EB + 16);
-      }
-#pragma unroll
-      for (int tj = 0; tj < 9; ++tj) {
-        sl = sl + 1 == Geo::NSL ? 0 : sl + 1;
-        if (tj < 8) {
-          const int f2b = sl * Geo::ROWB + lane_b;
-          bn[0] = tr_block(lds, f2b), bn[1] = tr_block(lds, f2b + 16);
-          bn[2] = tr_block(lds, f2b + Geo::EB), bn[3] = tr_block(lds, f2b + Geo::EB + 16);
-        }
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        const f32x4 d10 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bc[0], z, 0, 0, 0);
-        const f32x4 d20 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bc[1], z, 0, 0, 0);
-        const f32x4 d11 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bc[2], z, 0, 0, 0);
-        const f32x4 d21 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bc[3], z, 0, 0, 0);
-        const f32x4 e0 = diag(d10, d20, lo_half) * inv_divisor;  // exact: 2^-k
-        const f32x4 e1 = diag(d11, d21, lo_half) * inv_divisor;
-        u32x4 h;
-        if (plain) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            h[v] = __builtin_bit_cast(uint32_t, h2_t{(_Float16)e0[v], (_Float16)e1[v]});
-        } else {
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            h[v] = __builtin_bit_cast(uint32_t, h2_t{(_Float16)fmaxf(e0[v], e0[v] * slope),
-                                                     (_Float16)fmaxf(e1[v], e1[v] * slope)});
-        }
-        const uint32_t off = o0 + (uint32_t)((tj * 9 + jj) * H) * (uint32_t)W * 2u;
-        __builtin_amdgcn_raw_buffer_store_b128(h, rso, (int)(lane_ok ? off : kOOB), 0, POL);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) bc[k] = bn[k];
+      const uint32_t pstep = c.plane_b;
+      if constexpr (G::TS == 1) {
+        tj_rows<G, 0, 9>(lds, slot0, lane_b, a, lo_half, plain, inv_divisor, slope, rso, o0,
+                         pstep, lane_ok, jj);
+      } else {
+        if (th == 0)
+          tj_rows<G, 0, 5>(lds, slot0, lane_b, a, lo_half, plain, inv_divisor, slope, rso, o0,
+                           pstep, lane_ok, jj);
+        else
+          tj_rows<G, 5, 4>(lds, slot0, lane_b, a, lo_half, plain, inv_divisor, slope, rso, o0,
+                           pstep, lane_ok, jj);
       }
     }
-    slot0 = slot0 + 1 == Geo::NSL ? 0 : slot0 + 1;
+    slot0 = slot0 + 1 == G::NSL ? 0 : slot0 + 1;
   }
 }
 
-}  // namespace mstrip16
-
-// Whether the fp16 MFMA strip kernel serves this problem: fp16 storage, model.py:24's stride-2
-// displacements in raster order (dr = 4, pad = md, k = 1, s1 = 1: the caller), C = 32, W a
-// multiple of 8, 16-B aligned buffers, at least ~one workgroup per CU (knob mstrip16=0: off).
-bool corr_mstrip16_accepts(const void* in1, const void* in2, const void* out, int B, int C,
-                           int H, int W, int s2, int dtype, int layout) {
-  using G = mstrip16::Geo;
-  if (dtype != 1 || s2 != 2 || layout != kRaster || C != G::C) return false;
+template <class G>
+bool accepts(const void* in1, const void* in2, const void* out, int B, int H, int W) {
   if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16) return false;
-  if (W % 8 || W < 64 || H < 2 || (size_t)C * H * W * 2 >= 0x7ffffff0ull) return false;
+  if (W % 8 || W < 64 || H < 2 || (size_t)G::C * H * W * 2 >= 0x7ffffff0ull) return false;
   if ((size_t)81 * H * W * 2 >= 0x7ffffff0ull) return false;
-  if (debug_knob("mstrip16", 1) == 0) return false;
   const long long nblk = (long long)B * 2 * (((H + 1) / 2 + G::RCH - 1) / G::RCH) *
                          ((W + G::TW - 1) / G::TW);
   return nblk >= 192;
 }
 
+template <class G>
+hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int W, float inv,
+                  const OutEpi& epi, hipStream_t stream) {
+  const int nchunk = ((H + 1) / 2 + G::RCH - 1) / G::RCH;
+  const int ntx = (W + G::TW - 1) / G::TW;
+  const long long nblk = (long long)B * 2 * nchunk * ntx;
+  if (nblk <= 0) return hipSuccess;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_mstrip16<G>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
+  hipExtLaunchKernelGGL((corr_fwd_mstrip16<G>), dim3((unsigned)nblk), dim3(G::THREADS),
+                        G::LDS_BYTES, stream, ev0, ev1, 0, (const __half*)in1,
+                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, epi);
+  return hipGetLastError();
+}
+
+}  // namespace mstrip16
+
+// Whether the fp16 matrix-core strip kernel serves this problem: fp16 storage, model.py:24's
+// stride-2 displacements in raster order (dr = 4, pad = md, k = 1, s1 = 1: the caller), C = 32
+// (l4 geometry) or 64 (l3 geometry), W a multiple of 8, 16-B aligned buffers, at least ~one
+// workgroup per CU (knob mstrip16=0: off).
+bool corr_mstrip16_accepts(const void* in1, const void* in2, const void* out, int B, int C,
+                           int H, int W, int s2, int dtype, int layout) {
+  if (dtype != 1 || s2 != 2 || layout != kRaster) return false;
+  if (debug_knob("mstrip16", 1) == 0) return false;
+  if (C == 32) return mstrip16::accepts<mstrip16::GeoL4>(in1, in2, out, B, H, W);
+  if (C == 64) return mstrip16::accepts<mstrip16::GeoL3>(in1, in2, out, B, H, W);
+  return false;
+}
+
 hipError_t corr_forward_mstrip16(const void* in1, const void* in2, void* out, int B, int C,
                                  int H, int W, float divisor, hipStream_t stream) {
-  using G = mstrip16::Geo;
   if (!corr_mstrip16_accepts(in1, in2, out, B, C, H, W, 2, 1, kRaster))
     return hipErrorNotSupported;
   int ex;
@@ -355,24 +445,8 @@ hipError_t corr_forward_mstrip16(const void* in1, const void* in2, void* out, in
   const OutEpi epi = current_epi();
   if (!(epi.slope <= 1.f)) return hipErrorNotSupported;  // max(v, slope v) form
   if (epi.ostride % 8) return hipErrorNotSupported;      // 16-B stores
-  const int nchunk = ((H + 1) / 2 + G::RCH - 1) / G::RCH;
-  const int ntx = (W + G::TW - 1) / G::TW;
-  const long long nblk = (long long)B * 2 * nchunk * ntx;
-  if (nblk <= 0) return hipSuccess;
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&mstrip16::corr_fwd_mstrip16<2>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
-  hipExtLaunchKernelGGL((mstrip16::corr_fwd_mstrip16<2>), dim3((unsigned)nblk),
-                        dim3(G::THREADS), G::LDS_BYTES, stream, ev0, ev1, 0, (const __half*)in1,
-                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, epi);
-  return hipGetLastError();
+  if (C == 32) return mstrip16::launch<mstrip16::GeoL4>(in1, in2, out, B, H, W, inv, epi, stream);
+  return mstrip16::launch<mstrip16::GeoL3>(in1, in2, out, B, H, W, inv, epi, stream);
 }
 
 }  // namespace pwc

@@ -78,6 +78,11 @@ FWD = [
     ("corr9", torch.float16, (12, 32, 112, 256), "mstrip16, B=12"),
     ("corr9", torch.float16, (16, 32, 100, 200), "mstrip16, partial chunk and strip"),
     ("corr9", torch.float16, (24, 32, 99, 128), "mstrip16, odd height"),
+    # its C = 64 geometry (config-4 l3: 64-px strips, 7-row chunks, K = 64 as two MFMAs): the
+    # Sintel l3 shape, a partial last chunk with a partial strip, an odd height
+    ("corr9", torch.float16, (16, 64, 56, 128), "mstrip16 l3 geometry"),
+    ("corr9", torch.float16, (16, 64, 50, 96), "mstrip16 l3, partial chunk and strip"),
+    ("corr9", torch.float16, (16, 64, 55, 128), "mstrip16 l3, odd height"),
 ]
 
 
