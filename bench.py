@@ -79,7 +79,7 @@ CORR_ARGS = dict(pad_size=2 * SEARCH_RANGE + 1, kernel_size=1,
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PAIR_SEED = 20240601   # synthetic pair g of the checked set is seeded PAIR_SEED + g
 # the l4-sized correlation kernels (csrc/corr_strip.hip for fp32 C = 32, corr_stream.hip else)
-L4_KERNEL_RE = "corr_fwd_str(ip|eam)"
+L4_KERNEL_RE = "corr_fwd_(m?strip|stream)"
 CORR4_ARGS = dict(pad_size=SEARCH_RANGE, kernel_size=1, max_displacement=SEARCH_RANGE,
                   stride1=1, stride2=1)  # the north star's literal "d=4": displacements -4..4
 

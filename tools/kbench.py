@@ -118,6 +118,13 @@ def main():
                                   band=os.environ.get("PWC_DEBUG", ""), us=round(med, 2),
                                   min_us=round(mean, 2), gbs=round(fb / (med * 1e-6) / 1e9, 1),
                                   tag=args.tag)))
+        if "seq" in ops:
+            # the bench step's order at one level: the warp, then the correlation on its output
+            # (two launches; seq_us - warp_fwd us = the correlation behind a warp)
+            med, mean = timeit(lambda s: corr_forward(s["x1"], warp_forward(s["x2"], s["fl"]), 9,
+                                                      1, 9, 1, 2), sets, args.iters)
+            print(json.dumps(dict(level=l, op="warp_then_corr", shape=[B, C, h, w],
+                                  us=round(med, 2), min_us=round(mean, 2), tag=args.tag)))
         if "upwarp" in ops and h % 2 == 0 and w % 2 == 0:
             # model.py:78 + :80: fused flow upsample -> warp (flow_up emitted) against the
             # unfused ATen upsample * 2 followed by the warp kernel
