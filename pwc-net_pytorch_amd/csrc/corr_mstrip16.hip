@@ -22,10 +22,12 @@
 // fall on distinct 8-dword bank groups).  The loader de-interleaves the parities (one 16-B load =
 // 8 pixels of one channel -> 4 even + 4 odd halves, two v_perm each) and writes two 8-B runs.
 //
-// Diagonal extraction.  Lane l holds D[4(l>>4) + v][l & 15], v = 0..3.  Rows 0-7 come from the
-// first product, 8-15 from the second; within its 16-lane row of lanes, output ti of row i sits in
-// lane ti + (i mod 8), so two DPP row shifts per register (row_shl v on lane rows 0 and 2,
-// row_shl 4+v on rows 1 and 3) bring all four u of a lane row to lane ti.  With both parities,
+// Diagonal extraction.  Rows 0-7 need the u' block at u0-4, rows 8-15 the one at u0+4: with the
+// f1 operand split into its two row halves (the other half zeroed), both products accumulate
+// into ONE tile, D = A_lo B_1 + A_hi B_2.  Lane l holds D[4(l>>4) + v][l & 15], v = 0..3; within
+// its 16-lane row of lanes, output ti of row i sits in lane ti + (i mod 8), so two DPP row shifts
+// per register (row_shl v on lane rows 0 and 2, row_shl 4+v on rows 1 and 3) bring all four u of
+// a lane row to lane ti.  With both parities,
 // lane (g, ti) then holds 8 consecutive pixels of plane ti: one 16-B store.
 //
 // Schedule.  A workgroup owns a 128-px column strip of 14 parity rows, one output row per STEP:
@@ -33,8 +35,9 @@
 // m % 11) and f1 row s from one of two buffers.  Four loader waves keep the next TWO steps' rows
 // in flight in registers: between the barriers B_{s-1} and B_s they issue step s+2's loads and
 // write step s's (loaded two steps earlier) into the slot step s-3 freed, so a load has two steps
-// to land.  Four compute waves (one 16-u block each, both parities, all 9 tj) store each step's
-// row while the next steps compute.
+// to land.  Eight compute waves (a 16-u block and a share of the 9 displacement rows each, both
+// parities; two per SIMD, so one wave's MFMA and DPP latencies hide behind the other's) store
+// each step's row while the next steps compute.
 #include <hip/hip_ext.h>
 
 #include <cmath>
@@ -63,15 +66,15 @@ typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
 constexpr int row_halves(int nu) { return 2 * (16 * ((nu + 8 - 8 + 31) / 32) + 8); }
 
 // C channels, TW-px strips, RCH parity rows (steps) per workgroup.  Config-4 l4: <32, 128, 14>
-// (four 16-u blocks, one compute wave each); config-4 l3: <64, 64, 7> (two 16-u blocks, the 9
-// displacement rows split 5 + 4 over two waves each; K = 64 as two MFMAs per block).
+// (four 16-u blocks, the 9 displacement rows split 5 + 4 over two waves each); config-4 l3:
+// <64, 64, 7> (two 16-u blocks, rows split 3 + 2 + 2 + 2; K = 64 as two MFMAs per block).
 template <int C_, int TW_, int RCH_>
 struct Geo {
   static constexpr int C = C_, TW = TW_, RCH = RCH_;
   static constexpr int KC = C / 32;                // MFMA K chunks
   static constexpr int NU = TW / 2;                // pixels per parity
   static constexpr int NUB = NU / 16;              // 16-u blocks
-  static constexpr int TS = 4 / NUB;               // displacement-row splits per block
+  static constexpr int TS = 8 / NUB;               // displacement-row splits per block
   static constexpr int RS = row_halves(NU);
   static constexpr int EB = C * RS * 2;            // bytes per parity plane of a staged row
   static constexpr int ROWB = 2 * EB;              // bytes per staged row
@@ -88,7 +91,7 @@ struct Geo {
   static constexpr int NK2 = (IF2 + LT - 1) / LT;  // loader slots: f2 row, then f1 row
   static constexpr int NK1 = IF1 / LT;
   static constexpr int LB = NK2 + NK1;
-  static_assert(NWC == 4 && NUB * 16 == NU && C % 32 == 0, "four compute waves, 16-u blocks");
+  static_assert(NWC == 8 && NUB * 16 == NU && C % 32 == 0, "eight compute waves, 16-u blocks");
   static_assert((RS / 2) % 16 == 8 && RS >= NU + 8, "8 channel rows on distinct bank groups");
   static_assert(NK1 * LT == IF1, "f1 items fill the loader slots");
   static_assert(LDS_BYTES <= 160 * 1024 && THREADS <= 1024, "workgroup resources");
@@ -192,15 +195,32 @@ __device__ __forceinline__ int diag_reg(int t) {
   return __builtin_amdgcn_update_dpp(x, t, 0x104 + V, 0xA, 0xF, false);
 }
 
-__device__ __forceinline__ f32x4 diag(const f32x4& d1, const f32x4& d2, bool lo_half) {
-  const i32x4 a = __builtin_bit_cast(i32x4, d1), b = __builtin_bit_cast(i32x4, d2);
+__device__ __forceinline__ f32x4 diag(const f32x4& d) {
+  const i32x4 a = __builtin_bit_cast(i32x4, d);
   i32x4 r;
-  r[0] = diag_reg<0>(lo_half ? a[0] : b[0]);
-  r[1] = diag_reg<1>(lo_half ? a[1] : b[1]);
-  r[2] = diag_reg<2>(lo_half ? a[2] : b[2]);
-  r[3] = diag_reg<3>(lo_half ? a[3] : b[3]);
+  r[0] = diag_reg<0>(a[0]);
+  r[1] = diag_reg<1>(a[1]);
+  r[2] = diag_reg<2>(a[2]);
+  r[3] = diag_reg<3>(a[3]);
   return __builtin_bit_cast(f32x4, r);
 }
+
+// The f1 operand with its rows 8-15 (lo = true) or 0-7 (lo = false) zeroed: rows 0-7 of the
+// volume come from the u' block at u0 - 4 and rows 8-15 from the block at u0 + 4, so
+// D = A_lo B_1 + A_hi B_2 accumulates both halves in one tile (row i = lane & 15 of A).
+__device__ __forceinline__ f16x8 rows_half(const f16x8& a, bool keep) {
+  const u32x4 v = __builtin_bit_cast(u32x4, a);
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  return __builtin_bit_cast(f16x8, keep ? v : z);
+}
+
+#ifdef PWC_CENSUS
+// measurement build only (make CENSUS=1): ablation mask from knob ms_abl -- 1: no operand reads,
+// products or diagonals (zeros stored), 2: no stores, 4: the loader stages nothing after step 0
+#define MS_ABL(bit) (abl & (bit))
+#else
+#define MS_ABL(bit) 0
+#endif
 
 // The operand blocks of one displacement row: [parity][u' block][K chunk]
 template <class G>
@@ -223,10 +243,18 @@ __device__ __forceinline__ void read_b(const char* lds, int f2b, BOps<G>& b) {
 // read while this row's products, diagonals and store run.
 template <class G, int TJ0, int NTJ>
 __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
-                                        const f16x8 (&a)[2][G::KC], bool lo_half, bool plain,
+                                        const f16x8 (&a)[2][2][G::KC], bool plain,
                                         float inv_divisor, float slope,
                                         __amdgpu_buffer_rsrc_t rso, uint32_t o0, uint32_t pstep,
-                                        bool lane_ok, int jj) {
+                                        bool lane_ok, int jj, int abl) {
+  if (MS_ABL(1)) {
+    const u32x4 h = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int t = 0; t < NTJ; ++t)
+      __builtin_amdgcn_raw_buffer_store_b128(
+          h, rso, (int)(lane_ok ? o0 + (uint32_t)((TJ0 + t) * 9 + jj) * pstep : kOOB), 0, 2);
+    return;
+  }
   int sl = slot0 + TJ0;
   sl = sl >= G::NSL ? sl - G::NSL : sl;
   BOps<G> bc, bn;
@@ -236,17 +264,19 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
     const int tj = TJ0 + t;
     sl = sl + 1 == G::NSL ? 0 : sl + 1;
     if (t + 1 < NTJ) read_b<G>(lds, sl * G::ROWB + lane_b, bn);
+    // both parities' tiles interleaved: consecutive MFMAs are independent
+    f32x4 d[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int k = 0; k < G::KC; ++k)
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int pe = 0; pe < 2; ++pe)
+          d[pe] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[pe][hb][k], bc.v[pe][hb][k], d[pe], 0,
+                                                         0, 0);
     f32x4 e[2];
 #pragma unroll
-    for (int pe = 0; pe < 2; ++pe) {
-      f32x4 d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < G::KC; ++k) {
-        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[pe][k], bc.v[pe][0][k], d1, 0, 0, 0);
-        d2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[pe][k], bc.v[pe][1][k], d2, 0, 0, 0);
-      }
-      e[pe] = diag(d1, d2, lo_half) * inv_divisor;  // exact: 2^-k
-    }
+    for (int pe = 0; pe < 2; ++pe) e[pe] = diag(d[pe]) * inv_divisor;  // exact: 2^-k
     u32x4 h;
     if (plain) {
 #pragma unroll
@@ -268,7 +298,7 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
 template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
     const __half* __restrict__ in1, const __half* __restrict__ in2, __half* __restrict__ out,
-    int H, int W, int nchunk, int ntx, float inv_divisor, OutEpi epi) {
+    int H, int W, int nchunk, int ntx, float inv_divisor, OutEpi epi, int abl) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // logical block = (n, row parity, chunk, strip), strip fastest (XCD neighbours share rows)
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -334,7 +364,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
     for (int s = 1; s < G::RCH; ++s) {
       // between B_{s-1} and B_s (step s-1 computing): step s+2's loads out, step s's rows in
       // (f2 row s+8 into the slot of row s-3, f1 into buffer s & 1, both last read by step s-2)
-      if (s + 2 < G::RCH) step_issue<G>(c, it, s + 2, r[(s + 2) % 3]);
+      if (s + 2 < G::RCH && !MS_ABL(4)) step_issue<G>(c, it, s + 2, r[(s + 2) % 3]);
       step_write<G>(lds, it, s, r[s % 3]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // B_s
@@ -347,9 +377,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
   const int th = wave / G::NUB;  // displacement-row split
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, jj = lane & 15;
   const int lane_b = ((4 * g + q) * G::RS + 4 * p) * 2 + 32 * ub;
-  const bool lo_half = lane < 32;
+  const bool lo_rows = (lane & 15) < 8;  // A rows 0-7 (lanes l & 15 < 8)
   const int xs = c.x0 + 32 * ub + 8 * g;  // this lane's 8 output pixels
-  const bool lane_ok = jj < 9 && xs < W;
+  const bool lane_ok = jj < 9 && xs < W && !MS_ABL(2);
   const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * H * W)), (short)0,
       (int)(81u * c.plane_b), 0x00020000);
@@ -362,25 +392,38 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
     const int y = 2 * (c.Y0 + s) + py;
     if (y < H) {
       const int f1b = (G::NSL + (s & 1)) * G::ROWB + lane_b;
-      f16x8 a[2][G::KC];
+      f16x8 a[2][2][G::KC];  // [parity][rows 0-7 | rows 8-15][K chunk]
 #pragma unroll
       for (int e = 0; e < 2; ++e)
 #pragma unroll
-        for (int k = 0; k < G::KC; ++k)
-          a[e][k] = tr_block<G>(lds, f1b + e * G::EB + k * 32 * G::RS * 2);
+        for (int k = 0; k < G::KC; ++k) {
+          const f16x8 v = tr_block<G>(lds, f1b + e * G::EB + k * 32 * G::RS * 2);
+          a[e][0][k] = rows_half(v, lo_rows);
+          a[e][1][k] = rows_half(v, !lo_rows);
+        }
       const uint32_t o0 = ((uint32_t)y * W + xs) * 2u;
       const uint32_t pstep = c.plane_b;
-      if constexpr (G::TS == 1) {
-        tj_rows<G, 0, 9>(lds, slot0, lane_b, a, lo_half, plain, inv_divisor, slope, rso, o0,
-                         pstep, lane_ok, jj);
-      } else {
+      // the 9 displacement rows split over TS waves per block: 5 + 4, or 3 + 2 + 2 + 2
+#define PWC_TJ(A, N)                                                                          \
+  tj_rows<G, A, N>(lds, slot0, lane_b, a, plain, inv_divisor, slope, rso, o0, pstep,         \
+                   lane_ok, jj, abl)
+      if constexpr (G::TS == 2) {
         if (th == 0)
-          tj_rows<G, 0, 5>(lds, slot0, lane_b, a, lo_half, plain, inv_divisor, slope, rso, o0,
-                           pstep, lane_ok, jj);
+          PWC_TJ(0, 5);
         else
-          tj_rows<G, 5, 4>(lds, slot0, lane_b, a, lo_half, plain, inv_divisor, slope, rso, o0,
-                           pstep, lane_ok, jj);
+          PWC_TJ(5, 4);
+      } else {
+        static_assert(G::TS == 4, "tj splits");
+        if (th == 0)
+          PWC_TJ(0, 3);
+        else if (th == 1)
+          PWC_TJ(3, 2);
+        else if (th == 2)
+          PWC_TJ(5, 2);
+        else
+          PWC_TJ(7, 2);
       }
+#undef PWC_TJ
     }
     slot0 = slot0 + 1 == G::NSL ? 0 : slot0 + 1;
   }
@@ -411,11 +454,16 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+#ifdef PWC_CENSUS
+  const int abl = debug_knob("ms_abl", 0);
+#else
+  const int abl = 0;
+#endif
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
   hipExtLaunchKernelGGL((corr_fwd_mstrip16<G>), dim3((unsigned)nblk), dim3(G::THREADS),
                         G::LDS_BYTES, stream, ev0, ev1, 0, (const __half*)in1,
-                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, epi);
+                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, epi, abl);
   return hipGetLastError();
 }
 
