@@ -77,7 +77,8 @@ int main(int argc, char** argv) {
   }
   const size_t nin = (size_t)B * C * H * W, nout = (size_t)B * 81 * H * W;
   const size_t set_b = (2 * nin + nout) * 4;
-  const int NS = std::max(2, (int)((320ull << 20) / set_b) + 1);
+  const char* ns_env = std::getenv("STRIP_SETS");  // rotating buffer sets (default: past 320 MiB)
+  const int NS = ns_env ? std::max(1, std::atoi(ns_env)) : std::max(2, (int)((320ull << 20) / set_b) + 1);
   std::vector<float*> f1(NS), f2(NS), o1(NS), o2(NS);
   std::vector<float> h1(nin), h2(nin);
   uint32_t s = 12345;
