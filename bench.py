@@ -155,6 +155,12 @@ def parse_args(argv=None):
                     help="committed PMC summary used when the live passes cannot run")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 PMC passes for roofline.traffic")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 on GPUs: nccl (= RCCL, the production path) or gloo (rehearsal: "
+                         "the collectives run on CPU copies, the hot path on the GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsing the N > 1 launcher, sharding, "
+                         "broadcast and shard check on a one-GPU box; with --dist-backend gloo)")
     args = ap.parse_args(argv)
     if args.warmup is None:
         args.warmup = 2 if args.device == "cpu" else 300
@@ -519,7 +525,7 @@ def pair_checksums(s):
     return torch.stack(cols, 1)
 
 
-def shard_check(pass_, shapes, B, world, rank, dev, dtype):
+def shard_check(pass_, shapes, B, world, rank, dev, dtype, cdev=None):
     """Every rank computes its own pairs [rank*B, rank*B + B) of the checked set; rank 0
     gathers the per-pair checksums and compares them with its own computation of all
     world*B pairs (same batch composition -> bit-identical arithmetic)."""
@@ -528,8 +534,10 @@ def shard_check(pass_, shapes, B, world, rank, dev, dtype):
     pass_.full(s)
     cs = pair_checksums(s)
     if world > 1:
+        cs = cs.to(cdev or dev)
         parts = [torch.empty_like(cs) for _ in range(world)]
         dist.all_gather(parts, cs)
+        parts = [p.to(dev) for p in parts]
     else:
         parts = [cs]
     if rank != 0:
@@ -546,7 +554,8 @@ def shard_check(pass_, shapes, B, world, rank, dev, dtype):
 
 def broadcast_weights(dev):
     """one broadcast of the Net harness's weights from rank 0; every rank checks
-    it holds rank 0's parameters afterwards (checksums all_gathered)."""
+    it holds rank 0's parameters afterwards (checksums all_gathered).  `dev` is where the
+    collective runs: the GPU under RCCL, the CPU under the gloo rehearsal."""
     from pwcnet_amd.net import Net, NetArgs
     from pwcnet_amd.shard import broadcast_module
     torch.manual_seed(1000 + dist.get_rank())  # ranks start with different weights
@@ -848,10 +857,15 @@ def main(argv=None):
             print("bench.py: no HIP device (use --device cpu for the launcher rehearsal)",
                   file=sys.stderr)
             return 3
-        dev = torch.device("cuda", local)
+        dev = torch.device("cuda", 0 if args.same_device else local)
         torch.cuda.set_device(dev)
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
+            if args.dist_backend == "gloo":
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=dev)
+    # where the collectives run: the GPU under RCCL, CPU copies under gloo
+    cdev = dev if (cpu or args.dist_backend == "nccl") else torch.device("cpu")
     from pwcnet_amd.shard import all_ranks, max_over_ranks
 
     dtype = torch.float32 if args.dtype == "fp32" else torch.float16
@@ -859,7 +873,7 @@ def main(argv=None):
     B = args.batch
     shapes = level_shapes(args.height, args.width)
     fused = {int(v) for v in args.fused_levels.split(",") if v.strip()}
-    bcast = broadcast_weights(dev) if world > 1 else None
+    bcast = broadcast_weights(cdev) if world > 1 else None
 
     gpass = None
     if cpu:
@@ -975,7 +989,7 @@ def main(argv=None):
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
-        return max_over_ranks(el, device=dev), issued, all_ranks(el, device=dev)
+        return max_over_ranks(el, device=cdev), issued, all_ranks(el, device=cdev)
 
     def self_check(stepf, p):
         """Poison one set's outputs, run one step, compare every level with a fresh eager
@@ -993,7 +1007,7 @@ def main(argv=None):
         tol = 1e-5 if dtype == torch.float32 else 2e-3
         ok = all(d <= tol for d in diff)
         if world > 1:
-            flag = torch.tensor([int(ok)], device=dev)
+            flag = torch.tensor([int(ok)], device=cdev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             ok = bool(flag.item())
         return ok, diff
@@ -1019,7 +1033,7 @@ def main(argv=None):
             "replay": g_ok, "replay_max_rel_diff": g_diff,
         }
         replay_ok = replay_ok and g_ok
-    shards = shard_check(pass_, shapes, B, world, rank, dev, dtype)
+    shards = shard_check(pass_, shapes, B, world, rank, dev, dtype, cdev)
 
     C4, h4, w4 = shapes[-1]
     pairs = B * args.steps * world
@@ -1060,7 +1074,10 @@ def main(argv=None):
             "height": args.height,
             "width": args.width,
             "levels": [list(x) for x in shapes],
-            "parallelism": f"dp{world} (batch-sharded replicas, no data-path collective)",
+            "parallelism": (f"dp{world} (batch-sharded replicas, no data-path collective)"
+                            if not args.same_device else
+                            f"REHEARSAL: {world} ranks on one GPU over {args.dist_backend} "
+                            "(launcher, sharding, broadcast and shard check; not a scaling run)"),
             "buffer_sets": nsets,
             "fused_levels": sorted(fused),
             "order": "dependency (level after level; warp before correlation within a level)",
