@@ -276,3 +276,25 @@ def test_warp_backward_short_workspace_falls_back():
         _check(out, ref, torch.float32, bwd=True)
     torch.testing.assert_close(gx, dx, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(gf, df, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("case", ["aligned", "odd_offset", "odd_total"])
+def test_warp_fp16_alignment(case):
+    """fp16 warp (modules.py:31-42) on an aligned tensor, a tensor whose storage starts 2 bytes
+    past an aligned address (bit-identical to the aligned copy) and an odd element count, within
+    fp16 rounding of the oracle; flows reach past every border (N(0, 6^2) px)."""
+    from pwcnet_amd.ops import warp_forward
+    shape = (1, 3, 5, 7) if case == "odd_total" else (2, 8, 20, 36)
+    x, xn = _rand(shape, torch.float16, "px", case)
+    f, fn = _rand((shape[0], 2) + shape[2:], torch.float16, "pf", case, scale=6.0)
+    if case == "odd_offset":  # same values, storage starting 2 bytes past an aligned address
+        buf = torch.empty(x.numel() + 1, device=DEV, dtype=torch.float16)
+        xv = buf[1:].view(shape)
+        xv.copy_(x)
+        out = warp_forward(xv, f)
+    else:
+        out = warp_forward(x, f)
+    torch.cuda.synchronize()
+    _check(out, O.warp_forward(xn, fn), torch.float16)
+    if case == "odd_offset":
+        assert torch.equal(out, warp_forward(x, f))
