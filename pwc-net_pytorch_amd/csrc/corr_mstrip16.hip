@@ -67,15 +67,18 @@ constexpr int row_halves(int nu) { return 2 * (16 * ((nu + 8 - 8 + 31) / 32) + 8
 
 // C channels, TW-px strips, RCH parity rows (steps) per workgroup.  Config-4 l4: <32, 128, 14>
 // (four 16-u blocks, the 9 displacement rows split 5 + 4 over two waves each); config-4 l3:
-// <64, 64, 7> (two 16-u blocks, rows split 3 + 2 + 2 + 2; K = 64 as two MFMAs per block).
-template <int C_, int TW_, int RCH_>
+// <64, 64, 7> (two 16-u blocks, rows split 3 + 2 + 2 + 2; K = 64 as two MFMAs per block);
+// config-4 l2: <96, 32, 4, 24> (one 16-u block, rows split 2 + 1 x 7 over eight waves; K = 96
+// as three MFMAs; rows of 24 halves, NU + 8, so the ring fits the LDS -- at the cost of 2-way
+// bank conflicts on some transposed reads: RS_ overrides the conflict-free stride).
+template <int C_, int TW_, int RCH_, int RS_ = 0>
 struct Geo {
   static constexpr int C = C_, TW = TW_, RCH = RCH_;
   static constexpr int KC = C / 32;                // MFMA K chunks
   static constexpr int NU = TW / 2;                // pixels per parity
   static constexpr int NUB = NU / 16;              // 16-u blocks
   static constexpr int TS = 8 / NUB;               // displacement-row splits per block
-  static constexpr int RS = row_halves(NU);
+  static constexpr int RS = RS_ ? RS_ : row_halves(NU);
   static constexpr int EB = C * RS * 2;            // bytes per parity plane of a staged row
   static constexpr int ROWB = 2 * EB;              // bytes per staged row
   static constexpr int NSL = 11;                   // f2 ring: a step's 9 rows + 2 staged ahead
@@ -89,15 +92,16 @@ struct Geo {
   static constexpr int IF1 = C * G1;               // per f1 row
   static constexpr int LT = 64 * NWL;              // loader lanes
   static constexpr int NK2 = (IF2 + LT - 1) / LT;  // loader slots: f2 row, then f1 row
-  static constexpr int NK1 = IF1 / LT;
+  static constexpr int NK1 = (IF1 + LT - 1) / LT;
   static constexpr int LB = NK2 + NK1;
   static_assert(NWC == 8 && NUB * 16 == NU && C % 32 == 0, "eight compute waves, 16-u blocks");
-  static_assert((RS / 2) % 16 == 8 && RS >= NU + 8, "8 channel rows on distinct bank groups");
-  static_assert(NK1 * LT == IF1, "f1 items fill the loader slots");
+  static_assert((RS_ != 0 || (RS / 2) % 16 == 8) && RS >= NU + 8 && RS % 4 == 0,
+                "8 channel rows on distinct bank groups (unless overridden)");
   static_assert(LDS_BYTES <= 160 * 1024 && THREADS <= 1024, "workgroup resources");
 };
 using GeoL4 = Geo<32, 128, 14>;
 using GeoL3 = Geo<64, 64, 7>;
+using GeoL2 = Geo<96, 32, 4, 24>;
 
 constexpr uint32_t kOOB = 0x80000000u;
 
@@ -127,7 +131,7 @@ __device__ __forceinline__ void lane_items(const Ctx& c, int lt, LaneItems<G>& i
     const int per = f2 ? G::G2 : G::G1;
     const int ch = i / per, kk = i % per;
     const int x = f2 ? c.x0 - 8 + 8 * kk : c.x0 + 8 * kk;
-    const bool have = f2 ? i < G::IF2 : true;
+    const bool have = f2 ? i < G::IF2 : i < G::IF1;
     it.g[k] = have && x >= 0 && x < c.W ? (uint32_t)ch * c.plane_b + (uint32_t)x * 2u : kOOB;
     it.l[k] = have ? (ch * G::RS + 4 * kk) * 2 : -1;
   }
@@ -244,7 +248,7 @@ __device__ __forceinline__ void read_b(const char* lds, int f2b, BOps<G>& b) {
 template <class G, int TJ0, int NTJ>
 __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
                                         const f16x8 (&a)[2][2][G::KC], bool plain,
-                                        float inv_divisor, float slope,
+                                        float inv_divisor, float divisor, float slope,
                                         __amdgpu_buffer_rsrc_t rso, uint32_t o0, uint32_t pstep,
                                         bool lane_ok, int jj, int abl) {
   if (MS_ABL(1)) {
@@ -276,7 +280,13 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
                                                          0, 0);
     f32x4 e[2];
 #pragma unroll
-    for (int pe = 0; pe < 2; ++pe) e[pe] = diag(d[pe]) * inv_divisor;  // exact: 2^-k
+    for (int pe = 0; pe < 2; ++pe) {
+      // exact 2^-k multiply, or the reference's fp32 division when C is not a power of two
+      const f32x4 r = diag(d[pe]);
+      e[pe] = inv_divisor != 0.f ? r * inv_divisor
+                                 : f32x4{r[0] / divisor, r[1] / divisor, r[2] / divisor,
+                                         r[3] / divisor};
+    }
     u32x4 h;
     if (plain) {
 #pragma unroll
@@ -298,7 +308,7 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
 template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
     const __half* __restrict__ in1, const __half* __restrict__ in2, __half* __restrict__ out,
-    int H, int W, int nchunk, int ntx, float inv_divisor, OutEpi epi, int abl) {
+    int H, int W, int nchunk, int ntx, float inv_divisor, float divisor, OutEpi epi, int abl) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // logical block = (n, row parity, chunk, strip), strip fastest (XCD neighbours share rows)
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -405,13 +415,24 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
       const uint32_t pstep = c.plane_b;
       // the 9 displacement rows split over TS waves per block: 5 + 4, or 3 + 2 + 2 + 2
 #define PWC_TJ(A, N)                                                                          \
-  tj_rows<G, A, N>(lds, slot0, lane_b, a, plain, inv_divisor, slope, rso, o0, pstep,         \
+  tj_rows<G, A, N>(lds, slot0, lane_b, a, plain, inv_divisor, divisor, slope, rso, o0, pstep,\
                    lane_ok, jj, abl)
       if constexpr (G::TS == 2) {
         if (th == 0)
           PWC_TJ(0, 5);
         else
           PWC_TJ(5, 4);
+      } else if constexpr (G::TS == 8) {
+        switch (th) {
+          case 0: PWC_TJ(0, 2); break;
+          case 1: PWC_TJ(2, 1); break;
+          case 2: PWC_TJ(3, 1); break;
+          case 3: PWC_TJ(4, 1); break;
+          case 4: PWC_TJ(5, 1); break;
+          case 5: PWC_TJ(6, 1); break;
+          case 6: PWC_TJ(7, 1); break;
+          default: PWC_TJ(8, 1); break;
+        }
       } else {
         static_assert(G::TS == 4, "tj splits");
         if (th == 0)
@@ -441,6 +462,7 @@ bool accepts(const void* in1, const void* in2, const void* out, int B, int H, in
 
 template <class G>
 hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int W, float inv,
+                  float divisor,
                   const OutEpi& epi, hipStream_t stream) {
   const int nchunk = ((H + 1) / 2 + G::RCH - 1) / G::RCH;
   const int ntx = (W + G::TW - 1) / G::TW;
@@ -463,7 +485,7 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
   hipExtLaunchKernelGGL((corr_fwd_mstrip16<G>), dim3((unsigned)nblk), dim3(G::THREADS),
                         G::LDS_BYTES, stream, ev0, ev1, 0, (const __half*)in1,
-                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, epi, abl);
+                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, divisor, epi, abl);
   return hipGetLastError();
 }
 
@@ -471,7 +493,7 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int
 
 // Whether the fp16 matrix-core strip kernel serves this problem: fp16 storage, model.py:24's
 // stride-2 displacements in raster order (dr = 4, pad = md, k = 1, s1 = 1: the caller), C = 32
-// (l4 geometry) or 64 (l3 geometry), W a multiple of 8, 16-B aligned buffers, at least ~one
+// (l4 geometry), 64 (l3) or 96 (l2), W a multiple of 8, 16-B aligned buffers, at least ~one
 // workgroup per CU (knob mstrip16=0: off).
 bool corr_mstrip16_accepts(const void* in1, const void* in2, const void* out, int B, int C,
                            int H, int W, int s2, int dtype, int layout) {
@@ -479,6 +501,7 @@ bool corr_mstrip16_accepts(const void* in1, const void* in2, const void* out, in
   if (debug_knob("mstrip16", 1) == 0) return false;
   if (C == 32) return mstrip16::accepts<mstrip16::GeoL4>(in1, in2, out, B, H, W);
   if (C == 64) return mstrip16::accepts<mstrip16::GeoL3>(in1, in2, out, B, H, W);
+  if (C == 96) return mstrip16::accepts<mstrip16::GeoL2>(in1, in2, out, B, H, W);
   return false;
 }
 
@@ -488,13 +511,16 @@ hipError_t corr_forward_mstrip16(const void* in1, const void* in2, void* out, in
     return hipErrorNotSupported;
   int ex;
   const float mnt = std::frexp(divisor, &ex);
-  if (mnt != 0.5f) return hipErrorNotSupported;  // exact 1 / divisor multiply
-  const float inv = std::ldexp(1.f, 1 - ex);
+  // a power-of-two divisor is an exact multiply; otherwise the kernel divides (inv = 0)
+  const float inv = mnt == 0.5f ? std::ldexp(1.f, 1 - ex) : 0.f;
   const OutEpi epi = current_epi();
   if (!(epi.slope <= 1.f)) return hipErrorNotSupported;  // max(v, slope v) form
   if (epi.ostride % 8) return hipErrorNotSupported;      // 16-B stores
-  if (C == 32) return mstrip16::launch<mstrip16::GeoL4>(in1, in2, out, B, H, W, inv, epi, stream);
-  return mstrip16::launch<mstrip16::GeoL3>(in1, in2, out, B, H, W, inv, epi, stream);
+  if (C == 32) return mstrip16::launch<mstrip16::GeoL4>(in1, in2, out, B, H, W, inv, divisor, epi,
+                                                              stream);
+  if (C == 64) return mstrip16::launch<mstrip16::GeoL3>(in1, in2, out, B, H, W, inv, divisor, epi,
+                                                              stream);
+  return mstrip16::launch<mstrip16::GeoL2>(in1, in2, out, B, H, W, inv, divisor, epi, stream);
 }
 
 }  // namespace pwc

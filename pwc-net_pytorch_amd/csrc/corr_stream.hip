@@ -772,16 +772,17 @@ hipError_t corr_forward_mstrip16(const void*, const void*, void*, int, int, int,
 hipError_t corr_forward_stream(const void* in1, const void* in2, void* out, int B, int C, int H,
                                int W, int s2, int dtype, int layout, float divisor,
                                hipStream_t stream) {
+  // fp16 storage, C = 32 / 64 / 96 (config-4 l4 / l3 / l2): the matrix-core strip kernel
+  // (corr_mstrip16.hip), which also takes grids the stream kernel declines
+  if (corr_mstrip16_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)) {
+    const hipError_t e = corr_forward_mstrip16(in1, in2, out, B, C, H, W, divisor, stream);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (!corr_stream_accepts(in1, in2, out, B, C, H, W, s2, dtype)) return hipErrorNotSupported;
   // fp32 model-config grids of C = 32 (config 2 l4): the strip kernel (corr_strip.hip), whose
   // stores drain under compute; it declines what it does not serve
   if (corr_strip_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)) {
     const hipError_t e = corr_forward_strip(in1, in2, out, B, C, H, W, divisor, stream);
-    if (e != hipErrorNotSupported) return e;
-  }
-  // fp16 storage, C = 32 (config-4 l4): the matrix-core strip kernel (corr_mstrip16.hip)
-  if (corr_mstrip16_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)) {
-    const hipError_t e = corr_forward_mstrip16(in1, in2, out, B, C, H, W, divisor, stream);
     if (e != hipErrorNotSupported) return e;
   }
   const int twp = (W % 112 == 0 || W < 112) ? 112 : 128;  // column tile width in pixels

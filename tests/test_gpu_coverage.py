@@ -83,6 +83,11 @@ FWD = [
     ("corr9", torch.float16, (16, 64, 56, 128), "mstrip16 l3 geometry"),
     ("corr9", torch.float16, (16, 64, 50, 96), "mstrip16 l3, partial chunk and strip"),
     ("corr9", torch.float16, (16, 64, 55, 128), "mstrip16 l3, odd height"),
+    # its C = 96 geometry (config-4 l2: 32-px strips, 4-row chunks, K = 96 as three MFMAs,
+    # rows of 24 halves): the Sintel l2 shape, partial chunk and strip, odd height
+    ("corr9", torch.float16, (16, 96, 28, 64), "mstrip16 l2 geometry"),
+    ("corr9", torch.float16, (16, 96, 26, 56), "mstrip16 l2, partial chunk and strip"),
+    ("corr9", torch.float16, (16, 96, 27, 64), "mstrip16 l2, odd height"),
 ]
 
 
