@@ -59,8 +59,22 @@ extern "C" {
 /* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
  * 4: fused warp -> correlation, 5: fused flow upsample -> warp, corr into a slice,
  * 6: pwc_set_debug, 7: grouped warp / warp -> correlation launches, 8: one-launch warp
- * backward with a workspace). */
+ * backward with a workspace, 9: pwc_corr_forward_plan). */
 PWC_API int pwc_abi_version(void);
+
+/* Which kernel family pwc_corr_forward would launch for these arguments (the same dispatch
+ * predicates; no device call, no launch -- pointers are only inspected for alignment), for
+ * tests and measurement tools.  Returns -1 for arguments pwc_corr_forward rejects.  Replaces
+ * nothing in the reference (its launcher has one kernel, correlation_cuda_kernel.cu:348-359). */
+#define PWC_PLAN_OTHER 0    /* parity tiles / whole-half / generic kernels (corr_fwd.hip) */
+#define PWC_PLAN_STREAM 1   /* channel-streaming row bands (corr_stream.hip) */
+#define PWC_PLAN_BAND 2     /* all-channel band (warp_corr.hip, l0/l1) */
+#define PWC_PLAN_ROWS 3     /* row bands, channel chunks (corr_rows.hip, l2/l3) */
+#define PWC_PLAN_STRIP 4    /* fp32 stepped column strips (corr_strip.hip, l4) */
+#define PWC_PLAN_MSTRIP16 5 /* fp16 matrix-core strips (corr_mstrip16.hip) */
+PWC_API int pwc_corr_forward_plan(const void* in1, const void* in2, const void* out, int B,
+                                  int C, int H, int W, int pad_size, int kernel_size,
+                                  int max_displacement, int stride1, int stride2, int dtype);
 
 /* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
  * LDS-DMA kernel is launched with hipExtLaunchKernel, recording `start_event` / `stop_event`

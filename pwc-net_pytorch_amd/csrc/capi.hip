@@ -144,9 +144,39 @@ int force_generic() { return pwc::debug_knob("corr_path", 0); }
 
 }  // namespace
 
+namespace pwc {
+bool corr_strip_accepts(const void*, const void*, const void*, int, int, int, int, int, int, int);
+bool corr_mstrip16_accepts(const void*, const void*, const void*, int, int, int, int, int, int,
+                           int);
+}  // namespace pwc
+
 extern "C" {
 
-int pwc_abi_version(void) { return 8; }
+int pwc_abi_version(void) { return 9; }
+
+int pwc_corr_forward_plan(const void* in1, const void* in2, const void* out, int B, int C, int H,
+                          int W, int pad_size, int kernel_size, int max_displacement, int stride1,
+                          int stride2, int dtype) {
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W) ||
+      !corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo) ||
+      Ho <= 0 || Wo <= 0 || dtype < PWC_DTYPE_F32 || dtype > PWC_DTYPE_BF16)
+    return -1;
+  if (force_generic() != 0) return PWC_PLAN_OTHER;
+  const int path = pwc::corr_forward_path(in1, in2, out, B, C, H, W, pad_size, kernel_size,
+                                          max_displacement, stride1, stride2, pwc::kRaster,
+                                          dtype);
+  if (path == pwc::kPathBand) return PWC_PLAN_BAND;
+  if (path == pwc::kPathRows) return PWC_PLAN_ROWS;
+  if (path != pwc::kPathStream) return PWC_PLAN_OTHER;
+  // the order of corr_forward_stream (corr_stream.hip)
+  if (pwc::corr_mstrip16_accepts(in1, in2, out, B, C, H, W, stride2, dtype, pwc::kRaster))
+    return PWC_PLAN_MSTRIP16;
+  if (pwc::corr_strip_accepts(in1, in2, out, B, C, H, W, stride2, dtype, pwc::kRaster))
+    return PWC_PLAN_STRIP;
+  return PWC_PLAN_STREAM;
+}
 
 int pwc_set_debug(const char* spec) {
   pwc::debug_spec() = spec ? spec : "";
@@ -255,11 +285,19 @@ int pwc_corr_forward_into(const void* in1, const void* in2, void* out,
   if (dtype != PWC_DTYPE_F32 && dtype != PWC_DTYPE_F16 && dtype != PWC_DTYPE_BF16)
     return fail(fn, "unsupported dtype");
   hipError_t e = hipErrorNotSupported;
+  const long long epi_stride = ostride == vol ? 0 : ostride;
   if (dtype == PWC_DTYPE_F32 && force_generic() == 0) {  // kernels that write the slice directly
-    pwc::EpiScope scope(ostride == vol ? 0 : ostride, negative_slope);
+    pwc::EpiScope scope(epi_stride, negative_slope);
     e = pwc::corr_forward_t<float>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size, kernel_size,
                                    max_displacement, stride1, stride2, pwc::kRaster, divisor,
                                    nullptr, s, 0);
+  } else if (dtype == PWC_DTYPE_F16 && force_generic() == 0 && epi_stride % 8 == 0) {
+    // fp16: the matrix-core strip, stream and row-band kernels write the slice with 16-B
+    // stores of 8 halves, so an image stride that keeps them aligned (else: workspace + copy)
+    pwc::EpiScope scope(epi_stride, negative_slope);
+    e = pwc::corr_forward_t<__half>(in1, in2, out, B, C, H, W, Ho, Wo, pad_size, kernel_size,
+                                    max_displacement, stride1, stride2, pwc::kRaster, divisor,
+                                    nullptr, s, 0);
   }
   if (e != hipErrorNotSupported) return check_launch(fn, e);
   // dense volume in the workspace, then one strided copy applying the activation

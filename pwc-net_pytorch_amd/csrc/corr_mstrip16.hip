@@ -468,6 +468,7 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int
   const int ntx = (W + G::TW - 1) / G::TW;
   const long long nblk = (long long)B * 2 * nchunk * ntx;
   if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
     const hipError_t e =
@@ -494,11 +495,15 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int
 // Whether the fp16 matrix-core strip kernel serves this problem: fp16 storage, model.py:24's
 // stride-2 displacements in raster order (dr = 4, pad = md, k = 1, s1 = 1: the caller), C = 32
 // (l4 geometry), 64 (l3) or 96 (l2), W a multiple of 8, 16-B aligned buffers, at least ~one
-// workgroup per CU (knob mstrip16=0: off).
+// workgroup per CU, and an output epilogue the kernel writes itself (leaky_relu slope <= 1:
+// the max(v, slope v) form; a channel-slice stride that keeps 16-B stores aligned) -- so this
+// predicate, corr_forward_path and the launcher agree (knob mstrip16=0: off).
 bool corr_mstrip16_accepts(const void* in1, const void* in2, const void* out, int B, int C,
                            int H, int W, int s2, int dtype, int layout) {
   if (dtype != 1 || s2 != 2 || layout != kRaster) return false;
   if (debug_knob("mstrip16", 1) == 0) return false;
+  const OutEpi epi = current_epi();
+  if (!(epi.slope <= 1.f) || epi.ostride % 8) return false;
   if (C == 32) return mstrip16::accepts<mstrip16::GeoL4>(in1, in2, out, B, H, W);
   if (C == 64) return mstrip16::accepts<mstrip16::GeoL3>(in1, in2, out, B, H, W);
   if (C == 96) return mstrip16::accepts<mstrip16::GeoL2>(in1, in2, out, B, H, W);
@@ -513,9 +518,7 @@ hipError_t corr_forward_mstrip16(const void* in1, const void* in2, void* out, in
   const float mnt = std::frexp(divisor, &ex);
   // a power-of-two divisor is an exact multiply; otherwise the kernel divides (inv = 0)
   const float inv = mnt == 0.5f ? std::ldexp(1.f, 1 - ex) : 0.f;
-  const OutEpi epi = current_epi();
-  if (!(epi.slope <= 1.f)) return hipErrorNotSupported;  // max(v, slope v) form
-  if (epi.ostride % 8) return hipErrorNotSupported;      // 16-B stores
+  const OutEpi epi = current_epi();  // slope and stride checked by the predicate
   if (C == 32) return mstrip16::launch<mstrip16::GeoL4>(in1, in2, out, B, H, W, inv, divisor, epi,
                                                               stream);
   if (C == 64) return mstrip16::launch<mstrip16::GeoL3>(in1, in2, out, B, H, W, inv, divisor, epi,

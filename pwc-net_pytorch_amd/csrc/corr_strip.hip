@@ -464,6 +464,10 @@ bool corr_strip_accepts(const void* in1, const void* in2, const void* out, int B
   if (dtype != 0 || s2 != 2 || layout != kRaster || C != G::C) return false;
   if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16) return false;
   if (W % G::TW || H < 2 || (size_t)C * H * W * 4 >= 0x7ffffff0ull) return false;
+  // the 81-plane output is addressed through one 32-bit buffer resource whose out-of-range
+  // sentinel is 2^31: it must stay below that (larger grids go to the size_t stream kernel)
+  if ((size_t)81 * H * W * 4 >= 0x7ffffff0ull) return false;
+  if (!(current_epi().slope <= 1.f)) return false;  // the max(v, slope v) epilogue
   if (debug_knob("strip", 1) == 0) return false;
   const long long nblk = (long long)B * 2 * (((H + 1) / 2 + G::R - 1) / G::R) * (W / G::TW);
   return nblk >= 192;

@@ -50,6 +50,7 @@ class CorrProblem(ctypes.Structure):
 
 SYMBOLS = {
     "pwc_abi_version": (_I, []),
+    "pwc_corr_forward_plan": (_I, [_P, _P, _P] + [_I] * 10),
     "pwc_last_error": (ctypes.c_char_p, []),
     "pwc_time_next_corr": (_I, [_P, _P]),
     "pwc_set_debug": (_I, [ctypes.c_char_p]),
@@ -77,7 +78,7 @@ SYMBOLS = {
     "pwc_corr_forward_into": (_I, [_P, _P, _P, ctypes.c_longlong, ctypes.c_float] + [_I] * 11
                               + [_P, _Z, _P]),
 }
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lock = threading.Lock()
 _lib = None
@@ -125,6 +126,15 @@ def corr_output_shape(H, W, pad, k, md, s1, s2):
                                        ctypes.byref(oh), ctypes.byref(ow)),
           "Correlation")
     return oc.value, oh.value, ow.value
+
+
+PLAN_NAMES = {0: "other", 1: "stream", 2: "band", 3: "rows", 4: "strip", 5: "mstrip16"}
+
+
+def corr_forward_plan(B, C, H, W, pad, k, md, s1, s2, dtype=0, ptrs=(0x1000, 0x2000, 0x3000)):
+    """Kernel family pwc_corr_forward would launch (pwc_corr_forward_plan; no device call)."""
+    r = load().pwc_corr_forward_plan(*ptrs, B, C, H, W, pad, k, md, s1, s2, dtype)
+    return PLAN_NAMES.get(r, r)
 
 
 def set_debug(spec: str = "") -> None:

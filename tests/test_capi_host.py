@@ -217,3 +217,26 @@ def test_corr_group_entry_host_checks():
     assert lib.pwc_corr_forward_group(arr, 1, 9, 1, 9, 1, 0, 1, 0, None) == 0
     assert b"invalid correlation parameters" in lib.pwc_last_error()
     assert lib.pwc_corr_forward_group(None, 0, 9, 1, 9, 1, 2, 1, 0, None) == 1
+
+
+def test_corr_forward_plan_routes_and_declines():
+    """pwc_corr_forward_plan runs the dispatch predicates on the host: the config-2 / config-4
+    levels reach their kernels, and grids the 32-bit-addressed strip kernels cannot address
+    (an 81-plane output >= 2^31 bytes) fall through to the size_t stream kernel."""
+    from pwcnet_amd import _lib
+    plan = _lib.corr_forward_plan
+    c9 = (9, 1, 9, 1, 2)
+    assert plan(8, 32, 96, 112, *c9) == "strip"                # config 2 l4
+    assert plan(8, 64, 48, 56, *c9) == "rows"                  # config 2 l3
+    assert plan(8, 96, 24, 28, *c9) == "rows"                  # config 2 l2
+    assert plan(8, 192, 6, 7, *c9) == "band"                   # config 2 l0
+    assert plan(16, 32, 112, 256, *c9, dtype=1) == "mstrip16"  # config 4 l4
+    assert plan(16, 64, 56, 128, *c9, dtype=1) == "mstrip16"   # config 4 l3
+    assert plan(8, 32, 96, 112, 4, 1, 4, 1, 1) == "stream"     # Corr4 at l4
+    # H*W = 8.4 M px: input 1.07 GB (< 2^31, the strip would accept it), output 2.7 GB
+    assert plan(1, 32, 3000, 2800, *c9) == "stream"
+    assert plan(1, 32, 3000, 2800, *c9, dtype=1) == "mstrip16"  # fp16 output 1.36 GB < 2^31
+    assert plan(1, 32, 5000, 2800, *c9, dtype=1) == "stream"    # fp16 output 2.27 GB
+    assert plan(8, 32, 96, 112, *c9, ptrs=(0x1004, 0x2000, 0x3000)) != "strip"  # unaligned
+    assert plan(8, 32, 96, 112, 9, 1, 9, 1, 2, dtype=7) == -1
+    assert plan(8, 32, 96, 112, 9, 1, 9, 0, 2) == -1

@@ -131,8 +131,9 @@ def test_strip_into_cat_slice_leaky():
 
 
 def test_mstrip16_into_cat_slice_leaky():
-    """model.py:83-84 + :89/91 at config 4's l4 (fp16) through the matrix-core strip kernel: the
-    volume written into the cat buffer's slice with leaky_relu(0.1) fused, the rest untouched."""
+    """model.py:83-84 + :89/91 at config 4's l4 (fp16): the matrix-core strip kernel writes the
+    cat buffer's slice itself with leaky_relu(0.1) fused (its strided, activated epilogue); the
+    rest of the buffer untouched."""
     from pwcnet_amd.ops import corr_forward_into
     B, C, H, W = 12, 32, 112, 256
     a, an = _rand((B, C, H, W), torch.float16, "ma")
@@ -142,6 +143,27 @@ def test_mstrip16_into_cat_slice_leaky():
     torch.cuda.synchronize()
     ref = O.corr_forward(an, bn, 9, 1, 9, 1, 2)
     ref = np.where(ref > 0, ref, ref * 0.1)
+    _check(cat[:, C:C + 81], ref, torch.float16)
+    assert bool((cat[:, :C] == 7.0).all()) and bool((cat[:, C + 81:] == 7.0).all())
+
+
+@pytest.mark.parametrize("shape,extra", [((16, 64, 56, 128), 2), ((16, 96, 28, 64), 2),
+                                         ((4, 32, 112, 256), 3), ((16, 128, 14, 32), 2)])
+def test_fp16_into_cat_slice_strides(shape, extra):
+    """fp16 pwc_corr_forward_into at config 4's l3 / l2 (matrix-core strip, C = 64 / 96
+    geometries), l4 and l1 (row bands): the kernels write the slice directly with their fused
+    epilogue (image stride (C + 81 + extra) H W halves; these kernels need W % 8 == 0, so the
+    stride is always a multiple of the 8-half store).  Values against the oracle on the fp16
+    inputs, leaky_relu(0.01), the rest of the buffer untouched."""
+    from pwcnet_amd.ops import corr_forward_into
+    B, C, H, W = shape
+    a, an = _rand((B, C, H, W), torch.float16, "sa")
+    b, bn = _rand((B, C, H, W), torch.float16, "sb")
+    cat = torch.full((B, C + 81 + extra, H, W), 7.0, device=DEV, dtype=torch.float16)
+    corr_forward_into(a, b, cat[:, C:C + 81], 9, 1, 9, 1, 2, negative_slope=0.01)
+    torch.cuda.synchronize()
+    ref = O.corr_forward(an, bn, 9, 1, 9, 1, 2)
+    ref = np.where(ref > 0, ref, ref * 0.01)
     _check(cat[:, C:C + 81], ref, torch.float16)
     assert bool((cat[:, :C] == 7.0).all()) and bool((cat[:, C + 81:] == 7.0).all())
 

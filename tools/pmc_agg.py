@@ -16,18 +16,18 @@ def main():
     root = sys.argv[1]
     files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
     per = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(set)
+    disp = collections.defaultdict(set)  # (kernel, counter) -> dispatches that report it
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row.get("Kernel_Name", "?")[:90]
-                did = row.get("Dispatch_Id")
-                disp[k].add((f, did))
-                per[k][row["Counter_Name"]] += float(row["Counter_Value"])
+                c = row["Counter_Name"]
+                disp[(k, c)].add((f, row.get("Dispatch_Id")))
+                per[k][c] += float(row["Counter_Value"])
     for k, cs in per.items():
-        n = max(1, len(disp[k]))
-        print(json.dumps(dict(kernel=k, dispatches=n,
-                              **{c: round(v / n, 1) for c, v in sorted(cs.items())})))
+        n = max(len(disp[(k, c)]) for c in cs)
+        print(json.dumps(dict(kernel=k, dispatches=n, **{
+            c: round(v / max(1, len(disp[(k, c)])), 1) for c, v in sorted(cs.items())})))
     if "--delete" in sys.argv:
         for f in files:
             os.remove(f)
