@@ -48,18 +48,34 @@ namespace strip {
 #ifdef PWC_STRIP_CENSUS  // tools/strip_bench.hip only: per-workgroup phase stamps (100 MHz)
 // Stamps are kept in scalar registers and written once at the end of the wave: a global store
 // inside the loop would enter the compute waves' vmcnt accounting and distort the timing.
+// Layout per workgroup (64 slots): compute quad A (wave 0) 0..31, quad B (wave WPP) 32..63; in
+// each, slot 0 = entry, 1 = first data, 2 + 3 s + {0,1,2} = step s loop done / reduced / stores
+// issued; the loader's stamps are slots 61..63 of quad B's range (group 0, step-0 window, all).
 __device__ unsigned long long* g_census;
 #define STAMP(slot) (cen_t[(slot)] = __builtin_amdgcn_s_memrealtime())
-#define CENSUS_DECL unsigned long long cen_t[16] = {}
+// a runtime slot (the step loop): the stamp goes to LDS behind the window (a runtime index
+// into the stamp registers would put them in scratch; a global store would join the vmcnt
+// accounting).  Placed only where the wave has no LDS read in flight (after a step's loop).
+#define CSTAMP(slot)                                                                        \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                         \
+    const uint32_t a_ = lds0 + G::LDS_BYTES +                                               \
+                        (uint32_t)(((wave == 0 ? 0 : wave == G::WPP ? 32 : 64) + (slot)) * 8); \
+    asm volatile("ds_write_b64 %0, %1" ::"v"(a_), "v"(t_) : "memory");                     \
+  } while (0)
+#define CENSUS_DECL unsigned long long cen_t[32] = {}
 #define CENSUS_FLUSH(lo, hi, base)                                                     \
   do {                                                                                 \
     if ((threadIdx.x & 63) == 0 && g_census != nullptr)                                \
       for (int k_ = (lo); k_ < (hi); ++k_)                                             \
-        if (cen_t[k_]) g_census[blockIdx.x * 32 + (base) + k_] = cen_t[k_];            \
+        if (cen_t[k_]) g_census[blockIdx.x * 64 + (base) + k_] = cen_t[k_];            \
   } while (0)
 #else
 #define STAMP(slot) \
   do {              \
+  } while (0)
+#define CSTAMP(slot) \
+  do {               \
   } while (0)
 #define CENSUS_DECL \
   do {              \
@@ -71,35 +87,69 @@ __device__ unsigned long long* g_census;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int C_, int R_, int TW_>
+#ifndef PWC_STRIP_ABL
+#define PWC_STRIP_ABL 0
+#endif
+#ifndef PWC_STRIP_STORE_AUX  // output store cache policy (measurement builds may override)
+#define PWC_STRIP_STORE_AUX 2  // nontemporal
+#endif
+
+// C channels, R output parity rows per workgroup, TW-px column strips; the 9 x NSEG (tj, 4-px
+// segment) tasks of an output row split over TS workgroups (each stages only the f2 rows its tj
+// meet); NQD output rows per step (two compute waves each); LA channels of LDS read-ahead.
+// FULL: the strip is the whole image row (TW == W); a channel row then stages only its 2-quad
+// left halo (zeros) before its data, and its right halo is the next channel row's left halo,
+// so a row of all channels is 2 quads per channel shorter (+ 2 zero quads after the last).
+template <int C_, int R_, int TW_, int TS_ = 1, int NQD_ = 2, int LA_ = 1, bool FULL_ = false>
 struct Geo {
-  static constexpr int C = C_, R = R_, TW = TW_;
+  static constexpr int C = C_, R = R_, TW = TW_, TS = TS_, NQD = NQD_, LA = LA_;
+  static constexpr bool FULL = FULL_;
   static constexpr int CH = C / 2;          // channels per lane half
   static constexpr int NSEG = TW / 4;       // 4-px segments per strip row
-  static constexpr int QR = (TW + 16) / 4;  // quads per staged channel row (8-px halo each side)
-  static constexpr int ROWQ = C * QR;       // quads per staged f2 row (all channels)
+  // quads per staged channel row: 8-px halo each side (shared between channel rows if FULL)
+  static constexpr int QR = FULL ? TW / 4 + 2 : (TW + 16) / 4;
+  static constexpr int ROWQ = C * QR;       // quads per staged f2 row (all channels), DMA'd
   static constexpr int IPR = ROWQ / 64;     // LDS-DMAs per f2 row
-  // row stride in quads: = 14 (mod 16) makes the lane map's ds_read_b128 groups conflict-free
-  static constexpr int SIGMA = ROWQ + ((14 - ROWQ % 16) + 16) % 16;
-  static constexpr int NROW = R + 8;        // f2 parity rows of the strip
-  static constexpr int NQD = 2;             // compute quads (rows per step)
+  static constexpr int ZQ = FULL ? 2 : 0;   // zero quads after the DMA'd row (the last right halo)
+  // row stride in quads, = NSEG (mod 16): a lane's quad index is then its task index
+  // (tj NSEG + segment) + a constant, mod 16, so every ds_read_b128 lane group of 16
+  // consecutive-task lanes hits 16 distinct 16-B bank slots (conflict-free)
+  static constexpr int SIGMA = ROWQ + ZQ + ((NSEG % 16 - (ROWQ + ZQ) % 16) + 16) % 16;
+  static constexpr int NTASK_ALL = 9 * NSEG;  // (tj, segment) tasks per output row
+  static constexpr int NTASK = NTASK_ALL / TS;  // per workgroup of a task group
+  static constexpr int tj_lo(int g) { return g * NTASK / NSEG; }
+  static constexpr int tj_hi(int g) { return ((g + 1) * NTASK - 1) / NSEG; }
+  static constexpr int tj_span() {
+    int m = 0;
+    for (int g = 0; g < TS; ++g) m = tj_hi(g) - tj_lo(g) + 1 > m ? tj_hi(g) - tj_lo(g) + 1 : m;
+    return m;
+  }
+  static constexpr int TJS = tj_span();     // displacement rows a workgroup meets
+  static constexpr int NROW = R + TJS - 1;  // f2 parity rows of the strip
   static constexpr int NSTEP = R / NQD;
-  static constexpr int WIN = NQD + 8;       // f2 rows of step 0
-  static constexpr int NTASK = 9 * NSEG;    // (tj, segment) tasks per output row
-  static constexpr int WPP = (NTASK + 31) / 32;  // waves per quad (32 task slots each)
+  static constexpr int WIN = NQD + TJS - 1;  // f2 rows of step 0
+  static constexpr int WPP = (NTASK + 31) / 32;  // waves per output row (32 task slots each)
   static constexpr int NWC = WPP * NQD;     // compute waves
   static constexpr int THREADS = 64 * (NWC + 1);
   static constexpr int LDS_BYTES = NROW * SIGMA * 16;
+#ifdef PWC_STRIP_CENSUS
+  static constexpr int LDS_ALLOC = LDS_BYTES + 96 * 8;  // + the step stamps (census build)
+#else
+  static constexpr int LDS_ALLOC = LDS_BYTES;
+#endif
   static constexpr int NDMA = NROW * IPR;
   static constexpr int NBAR = IPR + NSTEP - 1;  // barriers every wave executes
   static_assert(C % 2 == 0 && TW % 4 == 0 && R % NQD == 0, "geometry");
+  static_assert(NTASK_ALL % TS == 0, "task groups");
   static_assert(ROWQ % 64 == 0, "a staged row is whole DMAs");
-  static_assert(LDS_BYTES <= 160 * 1024 && THREADS <= 1024, "workgroup resources");
-  // every read offset is an instruction immediate (16-bit)
-  static_assert(((NSTEP - 1) * NQD * SIGMA + (C - 2) * QR + 4) * 16 < 65536, "ds offsets");
+  static_assert(LDS_ALLOC <= 160 * 1024 && THREADS <= 1024, "workgroup resources");
+  static_assert(LA >= 1 && LA <= 2 && CH > LA, "read-ahead");
+  // every read offset inside a step is an instruction immediate (16-bit); the step's row base
+  // is in the address register
+  static_assert(((C - 2) * QR + 4) * 16 < 65536, "ds offsets");
 };
 
-// Loader DMA d -> (f2 row m, DMA i of the row): step 0's ten rows group-major (group i of all
+// Loader DMA d -> (f2 row m, DMA i of the row): step 0's rows group-major (group i of all
 // rows before group i + 1), then the later rows whole.
 template <class G>
 constexpr int dma_row(int d) {
@@ -142,7 +192,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 struct RowRsrc {
   const float* img;
   uint32_t img_bytes, row_bytes;
-  int Y0, py, H;
+  int P0, py, H;  // P0 = image parity row of staged row 0
 #ifdef PWC_STRIP_CENSUS
   unsigned long long* cen;
 #endif
@@ -153,7 +203,7 @@ __device__ __forceinline__ void dma_one(const RowRsrc& rr, const uint32_t (&rel)
                                         uint32_t lds0) {
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int m = dma_row<G>(D), i = dma_idx<G>(D);
-  const int pr = rr.Y0 - 4 + m;            // parity row of the image
+  const int pr = rr.P0 + m;                // parity row of the image
   const int yrow = 2 * pr + rr.py;         // image row
   const bool ok = pr >= 0 && yrow < rr.H;
   const uint32_t off = ok ? (uint32_t)yrow * rr.row_bytes : 0u;
@@ -186,9 +236,9 @@ __device__ __forceinline__ void loader_from(const RowRsrc& rr, const uint32_t (&
     dma_range<G, from, to>(rr, rel, lds0);
     wait_vmcnt<to - dma_need<G>(J)>();
 #ifdef PWC_STRIP_CENSUS
-    if constexpr (J == 0) rr.cen[13] = __builtin_amdgcn_s_memrealtime();  // group 0
-    if constexpr (J == G::IPR - 1) rr.cen[14] = __builtin_amdgcn_s_memrealtime();  // window
-    if constexpr (J == G::NBAR - 1) rr.cen[15] = __builtin_amdgcn_s_memrealtime();  // all rows
+    if constexpr (J == 0) rr.cen[29] = __builtin_amdgcn_s_memrealtime();  // group 0
+    if constexpr (J == G::IPR - 1) rr.cen[30] = __builtin_amdgcn_s_memrealtime();  // window
+    if constexpr (J == G::NBAR - 1) rr.cen[31] = __builtin_amdgcn_s_memrealtime();  // all rows
 #endif
     __builtin_amdgcn_s_barrier();
     loader_from<G, J + 1>(rr, rel, lds0);
@@ -219,15 +269,10 @@ __device__ __forceinline__ void lgk_wait(f32x4 (&w)[5]) {
                : "n"(N));
 }
 
-// v_permlane32_swap_b32 a, b: a's lanes 32-63 <-> b's lanes 0-31.  Written as asm: with ROCm
-// 7.2 the builtin's two results fold into one register when both feed one add (the sum read
-// v + v), dropping the other half.  The s_nops cover the VALU -> permlane operand hazard on
-// either side.
-__device__ __forceinline__ void swap32(float& a, float& b) {
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
-}
-// Four swaps in one block: one s_nop pair covers them (no swap reads a register another
-// writes).
+// Four v_permlane32_swap_b32 (a's lanes 32-63 <-> b's lanes 0-31) in one block: one s_nop
+// pair covers the VALU -> permlane operand hazard on either side (no swap reads a register
+// another writes).  Written as asm: with ROCm 7.2 the builtin's two results fold into one
+// register when both feed one add (the sum read v + v), dropping the other half.
 __device__ __forceinline__ void swap32x4(float& a0, float& b0, float& a1, float& b1, float& a2,
                                          float& b2, float& a3, float& b3) {
   asm volatile(
@@ -241,7 +286,7 @@ __device__ __forceinline__ void swap32x4(float& a0, float& b0, float& a1, float&
 }
 
 struct LaneCtx {
-  uint32_t addr;                   // LDS byte address of (row qd + tj, channel half, segment)
+  uint32_t addr;                   // LDS byte address of (step-0 row qd + tj - tj_lo, channel half, segment)
   __amdgpu_buffer_rsrc_t rs1;      // f1 of this image
   uint32_t f1off;                  // f1 voffset of step 0 (or kOOB)
   uint32_t f1step;                 // f1 voffset increment per step
@@ -251,35 +296,51 @@ struct LaneCtx {
 
 constexpr uint32_t kOOB = 0x80000000u;
 
+// f1 voffset of step st (kOOB: nothing to load -- zeros), computed once per step: a select
+// per channel load becomes a branch in the step loop, around which the compiler sinks the FMAs
 template <class G>
-__device__ __forceinline__ f32x4 load_f1(const LaneCtx& lc, int st, int k) {
-  const uint32_t v = st < lc.nstep_ok && lc.f1off != kOOB ? lc.f1off + (uint32_t)st * lc.f1step
-                                                          : kOOB;
+__device__ __forceinline__ uint32_t f1_voff(const LaneCtx& lc, int st) {
+  return st < lc.nstep_ok && lc.f1off != kOOB ? lc.f1off + (uint32_t)st * lc.f1step : kOOB;
+}
+template <class G>
+__device__ __forceinline__ f32x4 load_f1(const LaneCtx& lc, uint32_t v, int k) {
   return __builtin_bit_cast(
       f32x4, __builtin_amdgcn_raw_buffer_load_b128(lc.rs1, (int)v, (int)(k * lc.plane_b), 0));
 }
 
-// Channel k of step ST: barrier (step 0, when pair k+1 opens a DMA group), the next channel's
-// window reads, this channel's FMAs, the next step's f1 prefetch into f1[k].
-template <class G, int ST, int K>
-__device__ __forceinline__ void channel(const LaneCtx& lc, float (&acc)[9][4], f32x4 (&f1)[G::CH],
-                                        f32x4 (&wA)[5], f32x4 (&wB)[5]) {
+// Window buffer of channel k (LA + 1 rotating buffers)
+template <class G, int K>
+__device__ __forceinline__ f32x4 (&wbuf(f32x4 (&w)[G::LA + 1][5]))[5] {
+  return w[K % (G::LA + 1)];
+}
+
+// Issue channel K's window reads (step 0: after the barrier that lands its DMA group).
+template <class G, bool FIRST, int K>
+__device__ __forceinline__ void issue_read(uint32_t a, f32x4 (&w)[G::LA + 1][5]) {
+  if constexpr (FIRST && K > 0 && pair_group<G>(K) > pair_group<G>(K - 1))
+    __builtin_amdgcn_s_barrier();
+  read5<2 * K * G::QR * 16>(a, wbuf<G, K>(w));
+}
+
+// Channel k of a step (FIRST: step 0, whose window lands group by group; PF: the next step's
+// f1 is prefetched into f1[k]): the window reads of channel k + LA, wait for channel k's, its
+// FMAs, the prefetch.
+template <class G, bool FIRST, bool PF, int K>
+__device__ __forceinline__ void channel(const LaneCtx& lc, uint32_t f1v, uint32_t a, float (&acc)[9][4],
+                                        f32x4 (&f1)[G::CH], f32x4 (&w)[G::LA + 1][5]) {
   if constexpr (K < G::CH) {
-    f32x4(&cur)[5] = (K & 1) ? wB : wA;
-    f32x4(&nxt)[5] = (K & 1) ? wA : wB;
-    if constexpr (K + 1 < G::CH) {
-      if constexpr (ST == 0 && pair_group<G>(K + 1) > pair_group<G>(K))
-        __builtin_amdgcn_s_barrier();
-      constexpr int O = (ST * G::NQD * G::SIGMA + 2 * (K + 1) * G::QR) * 16;
-      read5<O>(lc.addr, nxt);
-      lgk_wait<5>(cur);
+    if constexpr (K + G::LA < G::CH) {
+      // PWC_STRIP_ABL 2: no window reads after step 0 (measurement only)
+      if constexpr (FIRST || !(PWC_STRIP_ABL & 2)) issue_read<G, FIRST, K + G::LA>(a, w);
+      lgk_wait<5 * G::LA>(wbuf<G, K>(w));
     } else {
-      lgk_wait<0>(cur);
+      lgk_wait<5 * (G::CH - 1 - K)>(wbuf<G, K>(w));
     }
-    corr_fma_pairs_s2<9, 5>(acc, f1[K], cur);
-    if constexpr (ST + 1 < G::NSTEP) f1[K] = load_f1<G>(lc, ST + 1, K);
+    // PWC_STRIP_ABL 4: no FMAs, 8: no f1 prefetch (measurement only)
+    if constexpr (!(PWC_STRIP_ABL & 4)) corr_fma_pairs_s2<9, 5>(acc, f1[K], wbuf<G, K>(w));
+    if constexpr (PF && !(PWC_STRIP_ABL & 8)) f1[K] = load_f1<G>(lc, f1v, K);
     __builtin_amdgcn_sched_barrier(0);
-    channel<G, ST, K + 1>(lc, acc, f1, wA, wB);
+    channel<G, FIRST, PF, K + 1>(lc, f1v, a, acc, f1, w);
   }
 }
 
@@ -288,15 +349,18 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
     int H, int W, int ngrp, int ntx, float inv_divisor, OutEpi epi) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  // logical block = (n, row parity, row group, strip), strip fastest: the strips of one image
-  // parity are neighbours and xcd_remap keeps neighbours on one XCD (shared f2 rows)
+  // logical block = (n, row parity, row group, strip, task group), task group fastest: the
+  // workgroups of one image parity are neighbours and xcd_remap keeps neighbours on one XCD
+  // (shared f2 rows)
   const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int tx = t % ntx;
-  const int grp = (t / ntx) % ngrp;
-  const int py = (t / (ntx * ngrp)) & 1;
-  const int n = t / (ntx * ngrp * 2);
+  const int tg = t % G::TS;
+  const int tx = (t / G::TS) % ntx;
+  const int grp = (t / (G::TS * ntx)) % ngrp;
+  const int py = (t / (G::TS * ntx * ngrp)) & 1;
+  const int n = t / (G::TS * ntx * ngrp * 2);
   const int Y0 = grp * G::R;  // first parity row of the group
   const int x0 = tx * G::TW;  // first pixel of the strip
+  const int tjlo = tg * G::NTASK / G::NSEG;  // first displacement row of the task group
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t plane_b = (uint32_t)(H * W) * 4u;
@@ -319,78 +383,93 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
       rel[i] = px >= 0 && px < W ? ((uint32_t)c * plane_b + (uint32_t)px * 4u) : kOOB;
     }
 #ifdef PWC_STRIP_CENSUS
-    const RowRsrc rr{img2, img_bytes, (uint32_t)W * 4u, Y0, py, H, cen_t};
+    const RowRsrc rr{img2, img_bytes, (uint32_t)W * 4u, Y0 - 4 + tjlo, py, H, cen_t};
 #else
-    const RowRsrc rr{img2, img_bytes, (uint32_t)W * 4u, Y0, py, H};
+    const RowRsrc rr{img2, img_bytes, (uint32_t)W * 4u, Y0 - 4 + tjlo, py, H};
 #endif
     loader_from<G, 0>(rr, rel, lds0);
-    CENSUS_FLUSH(13, 16, 0);
+    CENSUS_FLUSH(29, 32, 32);
     return;
   }
 
   // ---------------- compute waves ----------------
   const int qd = wave / G::WPP, wq = wave % G::WPP;
   const int slot = lane & 31, chalf = lane >> 5;
-  const int task = 32 * wq + slot;
-  const bool active = task < G::NTASK;
-  const int tt = active ? task : G::NTASK - 1;  // idle slots duplicate a lane of their group
+  const int gtask = 32 * wq + slot;               // task of this workgroup's group
+  const bool active = gtask < G::NTASK;
+  const int tt = tg * G::NTASK + (active ? gtask : G::NTASK - 1);  // idle slots duplicate a lane
   const int tj = tt / G::NSEG, seg = tt % G::NSEG;
   const int px = x0 + 4 * seg;
   LaneCtx lc;
-  lc.addr = lds0 + (uint32_t)(((qd + tj) * G::SIGMA + chalf * G::QR + seg) * 16);
+  lc.addr = lds0 + (uint32_t)(((qd + tj - tjlo) * G::SIGMA + chalf * G::QR + seg) * 16);
   lc.rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)img1, (short)0, (int)img_bytes, 0x00020000);
   const int yrow0 = 2 * (Y0 + qd) + py;  // this quad's output row in step 0
   lc.f1off = px < W ? ((uint32_t)(chalf * G::CH) * plane_b + ((uint32_t)yrow0 * W + px) * 4u)
                     : kOOB;
   lc.f1step = (uint32_t)(2 * G::NQD * W) * 4u;
   lc.plane_b = plane_b;
-  // steps whose output row (2 (Y0 + 2 st + qd) + py) lies inside the image
+  // steps whose output row (2 (Y0 + NQD st + qd) + py) lies inside the image
   lc.nstep_ok = yrow0 < H ? min(G::NSTEP, (H - 1 - yrow0) / (2 * G::NQD) + 1) : 0;
 
+  if constexpr (G::ZQ > 0) {
+    // the last channel row's right halo (never DMA'd): zero quads behind every staged row,
+    // written before step 0's first barrier
+    if (wave == 0 && lane < G::NROW * G::ZQ) {
+      const uint32_t za = lds0 + (uint32_t)(((lane / G::ZQ) * G::SIGMA + G::ROWQ + lane % G::ZQ) * 16);
+      asm volatile("ds_write_b128 %0, %1" ::"v"(za), "v"(f32x4{0.f, 0.f, 0.f, 0.f}) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   f32x4 f1[G::CH];
 #pragma unroll
-  for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, 0, k);
+  for (int k = 0; k < G::CH; ++k) f1[k] = load_f1<G>(lc, f1_voff<G>(lc, 0), k);
 
-  // output: one buffer resource over the image's 81 planes; a store whose lane has nothing to
-  // write (idle task, row or strip outside the image, the high half's fifth store) gets an
-  // out-of-range offset.  Every store instruction is then unconditional, so the compiler's
-  // vmcnt count for the f1 prefetch stays exact across steps (a branch around a store makes
-  // it assume the store-less path and wait for stores still draining).
+  // output: one buffer resource over the image's 81 planes (< 2^31 bytes: the accepts
+  // predicate); a store whose lane has nothing to write (idle task, row or strip outside the
+  // image, the high half's fifth store) gets an out-of-range offset.  Every store instruction
+  // is then unconditional, so the compiler's vmcnt count for the f1 prefetch stays exact across
+  // steps (a branch around a store makes it assume the store-less path and wait for stores
+  // still draining).
   float* oimg = out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * H * W);
   const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc(
       (void*)oimg, (short)0, (int)(81u * plane_b), 0x00020000);
   // leaky_relu (model.py:84) as max(v, slope v): equal to epi_act for slope <= 1 (the
-  // launcher declines larger slopes), and the identity at slope 1, bit for bit
+  // predicate declines larger slopes), and the identity at slope 1, bit for bit
   const float slope = epi.slope;
-  auto step = [&](auto st_c) {
-    constexpr int ST = decltype(st_c)::value;
+  // one step: rows 2 (Y0 + NQD st + qd) + py; step 0 and the last step unrolled, the steps in
+  // between one runtime loop body (an unrolled chain of steps lets the compiler stretch live
+  // ranges across them and spill)
+  auto step = [&](auto first_c, auto pf_c, int st) {
+    constexpr bool FIRST = decltype(first_c)::value, PF = decltype(pf_c)::value;
     float acc[9][4];
 #pragma unroll
     for (int a = 0; a < 9; ++a)
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[a][e] = 0.f;
-    f32x4 wA[5], wB[5];
+    f32x4 w[G::LA + 1][5];
+    const uint32_t a = lc.addr + (uint32_t)(st * G::NQD * G::SIGMA * 16);
     __builtin_amdgcn_s_barrier();  // step 0: group 0 landed; later steps: their rows landed
-    if (ST == 0) STAMP(1);
-    read5<ST * G::NQD * G::SIGMA * 16>(lc.addr, wA);
-    channel<G, ST, 0>(lc, acc, f1, wA, wB);
-    STAMP(2 + 3 * ST);  // loop done
+    if (FIRST) STAMP(1);
+    issue_read<G, FIRST, 0>(a, w);
+    if constexpr (G::LA > 1) issue_read<G, FIRST, 1>(a, w);
+    channel<G, FIRST, PF, 0>(lc, f1_voff<G>(lc, st + 1), a, acc, f1, w);
+    CSTAMP(2 + 3 * st);  // loop done
     // channel halves: lane l (c < C/2) and l + 32 (c >= C/2) hold partial sums of the same
     // task.  One v_permlane32_swap per pair (ti, ti + 5) leaves both halves of the pair in
     // each lane; their sum is displacement ti's total in one half and ti + 5's in the other.
     float res[5][4];
 #pragma unroll
     for (int ti = 0; ti < 5; ++ti) {
-      float a[4], b[4];
+      float x[4], y[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] = acc[ti][e], b[e] = ti < 4 ? acc[ti + 5][e] : acc[ti][e];
-      swap32x4(a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3]);
+      for (int e = 0; e < 4; ++e) x[e] = acc[ti][e], y[e] = ti < 4 ? acc[ti + 5][e] : acc[ti][e];
+      swap32x4(x[0], y[0], x[1], y[1], x[2], y[2], x[3], y[3]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) res[ti][e] = a[e] + b[e];
+      for (int e = 0; e < 4; ++e) res[ti][e] = x[e] + y[e];
     }
-    STAMP(3 + 3 * ST);  // channel halves reduced
-    const int yrow = yrow0 + 2 * G::NQD * ST;
-    const bool wr = active && px < W && ST < lc.nstep_ok;
+    CSTAMP(3 + 3 * st);  // channel halves reduced
+    const int yrow = yrow0 + 2 * G::NQD * st;
+    const bool wr = active && px < W && st < lc.nstep_ok;
     // the swap pairs (ti, ti + 5): the low half keeps ti, the high half ti + 5
     const uint32_t o0 = (uint32_t)(((tj * 9 + 5 * chalf) * H + yrow) * W + px) * 4u;
     const uint32_t ostep = plane_b;  // next displacement plane
@@ -403,19 +482,30 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
         const float o = res[q][e] * inv_divisor;  // exact: the divisor is a power of two
         v[e] = __builtin_bit_cast(uint32_t, fmaxf(o, o * slope));
       }
-      const bool ok = wr && (q < 4 || chalf == 0);
+      // measurement builds (tools/strip_bench, -DPWC_STRIP_ABL=mask): 1 = stores discarded
+      const bool ok = !(PWC_STRIP_ABL & 1) && wr && (q < 4 || chalf == 0);
       // nontemporal (aux 2): measured against sc1, nt sc1 and plain stores, 14.2 against
       // 17.0-19.9 us back to back (profiles/r04a_strip_store_policy.txt)
-      __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0,
+                                             PWC_STRIP_STORE_AUX);
     }
-    STAMP(4 + 3 * ST);  // stores issued
+    CSTAMP(4 + 3 * st);  // stores issued
   };
-  step(std::integral_constant<int, 0>{});
-  if constexpr (G::NSTEP > 1) step(std::integral_constant<int, 1>{});
-  if constexpr (G::NSTEP > 2) step(std::integral_constant<int, 2>{});
-  static_assert(G::NSTEP <= 3, "unrolled steps");
-  if (wave == 0) CENSUS_FLUSH(0, 11, 0);
-  if (wave == G::WPP) CENSUS_FLUSH(0, 11, 16);  // the second quad's first wave
+  step(std::true_type{}, std::integral_constant<bool, (G::NSTEP > 1)>{}, 0);
+#pragma unroll 1
+  for (int st = 1; st < G::NSTEP - 1; ++st) step(std::false_type{}, std::true_type{}, st);
+  if constexpr (G::NSTEP > 1) step(std::false_type{}, std::false_type{}, G::NSTEP - 1);
+#ifdef PWC_STRIP_CENSUS
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  {
+    const unsigned long long* st_ = reinterpret_cast<const unsigned long long*>(
+        reinterpret_cast<const char*>(lds) + G::LDS_BYTES);
+    const int b_ = wave == 0 ? 0 : 32;
+    for (int k_ = 2; k_ < 2 + 3 * G::NSTEP; ++k_) cen_t[k_] = st_[b_ + k_];
+  }
+#endif
+  if (wave == 0) CENSUS_FLUSH(0, 2 + 3 * G::NSTEP, 0);
+  if (wave == G::WPP) CENSUS_FLUSH(0, 2 + 3 * G::NSTEP, 32);  // the second quad's first wave
 }
 
 template <class G>
@@ -424,14 +514,14 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   const int hp0 = (H + 1) / 2;  // parity-0 rows (the larger parity)
   const int ngrp = (hp0 + G::R - 1) / G::R;
   const int ntx = (W + G::TW - 1) / G::TW;
-  const long long nblk = (long long)B * 2 * ngrp * ntx;
+  const long long nblk = (long long)B * 2 * ngrp * ntx * G::TS;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_strip<G>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             G::LDS_BYTES);
+                                             G::LDS_ALLOC);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -444,20 +534,34 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
   hipExtLaunchKernelGGL((corr_fwd_strip<G>), dim3((unsigned)nblk), dim3(G::THREADS),
-                        G::LDS_BYTES, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,
+                        G::LDS_ALLOC, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,
                         (float*)out, H, W, ngrp, ntx, inv, epi);
   return hipGetLastError();
 }
 
+template <class G>
+long long grid_blocks(int B, int H, int W) {
+  return (long long)B * 2 * (((H + 1) / 2 + G::R - 1) / G::R) * ((W + G::TW - 1) / G::TW) * G::TS;
+}
+
+// 6 parity rows x 56-px strips per workgroup, all 9 displacement rows (14 staged f2 rows):
+// widths that are other multiples of 56 (the 224-px stress shape)
 using GeoL4 = Geo<32, 6, 56>;
+// W = 112 (config 2 l4): whole 112-px rows, so every store of a displacement plane covers a
+// whole 448-B image row (the 56-px strips left the 128-B lines at the strip seam and across
+// the row-parity seam half-written by two workgroups: 7.2 against 5.9 us for the volume's
+// stores alone, tools/store_probe.hip); 6 parity rows, the (tj, segment) tasks of a row split
+// over two workgroups (10 staged f2 rows each)
+using GeoF = Geo<32, 6, 112, 2, 2, 1, true>;
 
 }  // namespace strip
 
 // Whether the strip kernel serves this problem: fp32, model.py:24's stride-2 displacements in
 // raster order (dr = 4, pad = md, k = 1, s1 = 1: checked by the caller), C = 32, W a multiple
-// of the 56-px strip, 16-B aligned buffers, and at least about one workgroup per CU (smaller
-// grids leave CUs idle: the stream kernel's 3-row bands suit them better).  Knob strip=0
-// disables it (measurement of the stream kernel).
+// of the 56-px strip, 16-B aligned buffers, an output the kernel's 32-bit buffer addressing
+// reaches, the max(v, slope v) epilogue, and at least about one workgroup per CU (smaller grids
+// leave CUs idle: the stream kernel's 3-row bands suit them better).  Knob strip=0 disables it
+// (measurement of the stream kernel); strip_geo=4 selects the 56-px strips at W = 112.
 bool corr_strip_accepts(const void* in1, const void* in2, const void* out, int B, int C, int H,
                         int W, int s2, int dtype, int layout) {
   using G = strip::GeoL4;
@@ -469,13 +573,16 @@ bool corr_strip_accepts(const void* in1, const void* in2, const void* out, int B
   if ((size_t)81 * H * W * 4 >= 0x7ffffff0ull) return false;
   if (!(current_epi().slope <= 1.f)) return false;  // the max(v, slope v) epilogue
   if (debug_knob("strip", 1) == 0) return false;
-  const long long nblk = (long long)B * 2 * (((H + 1) / 2 + G::R - 1) / G::R) * (W / G::TW);
-  return nblk >= 192;
+  return strip::grid_blocks<G>(B, H, W) >= 192;
 }
 
 hipError_t corr_forward_strip(const void* in1, const void* in2, void* out, int B, int C, int H,
                               int W, float divisor, hipStream_t stream) {
   if (!corr_strip_accepts(in1, in2, out, B, C, H, W, 2, 0, kRaster)) return hipErrorNotSupported;
+  // whole rows where the width is the full-row geometry's (knob strip_geo=4: the 56-px strips)
+  if (W == strip::GeoF::TW && debug_knob("strip_geo", 5) != 4 &&
+      strip::grid_blocks<strip::GeoF>(B, H, W) >= 192)
+    return strip::launch<strip::GeoF>(in1, in2, out, B, H, W, divisor, stream);
   return strip::launch<strip::GeoL4>(in1, in2, out, B, H, W, divisor, stream);
 }
 

@@ -67,10 +67,13 @@ FWD = [
     ("corr9", torch.float16, (4, 32, 192, 224), "stream<half,2,3,112>"),
     ("corr4", torch.float16, (4, 32, 192, 224), "stream<half,1,3,112>"),
     ("corr4", torch.float16, (2, 32, 192, 224), "stream<half,1,4,112>"),
-    # the strip kernel (corr_strip.hip): the smallest batch it takes, a partial last row group
-    # (H = 90: 45 parity rows in groups of 6), four strips per row (W = 224)
-    ("corr9", torch.float32, (6, 32, 96, 112), "strip, B=6"),
-    ("corr9", torch.float32, (8, 32, 90, 112), "strip, partial row group"),
+    # the strip kernel (corr_strip.hip), full-row geometry at W = 112 (GeoF: two task groups,
+    # shared channel-row halos): the smallest batch it takes, a partial last row group (H = 90:
+    # 45 parity rows in groups of 6), an odd height (parity rows 48 / 47); the 56-px strips
+    # (GeoL4) at W = 224: four strips per row
+    ("corr9", torch.float32, (6, 32, 96, 112), "strip full rows, B=6"),
+    ("corr9", torch.float32, (8, 32, 90, 112), "strip full rows, partial row group"),
+    ("corr9", torch.float32, (8, 32, 95, 112), "strip full rows, odd height"),
     ("corr9", torch.float32, (4, 32, 192, 224), "strip, 4 strips per row"),
     # the matrix-core fp16 strip kernel (corr_mstrip16.hip): its smallest batch at Sintel l4, a
     # partial last chunk (50 parity rows in chunks of 14) with a partial last strip (W = 200),
@@ -100,6 +103,26 @@ def test_corr_forward_reached_instantiations(cfg, dtype, shape, what):
     out = corr_forward(a, b, *CFG[cfg])
     torch.cuda.synchronize()
     _check(out, O.corr_forward(an, bn, *CFG[cfg]), dtype)
+
+
+@pytest.mark.parametrize("shape", [(8, 32, 96, 112), (8, 32, 91, 112)], ids=["l4", "odd"])
+def test_strip_56px_geometry_at_w112(shape):
+    """The 56-px strip geometry (GeoL4) at config 2's width, selected by the knob strip_geo=4
+    (the full-row geometry is the default there): equal to the oracle, and to the default
+    geometry bit for bit (same per-element fp32 order of the channel sum)."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_forward
+    a, an = _rand(shape, torch.float32, "g4a", shape)
+    b, bn = _rand(shape, torch.float32, "g4b", shape)
+    ref = corr_forward(a, b, 9, 1, 9, 1, 2)
+    _lib.set_debug("strip_geo=4")
+    try:
+        out = corr_forward(a, b, 9, 1, 9, 1, 2)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_debug("")
+    _check(out, O.corr_forward(an, bn, 9, 1, 9, 1, 2), torch.float32)
+    assert torch.equal(out, ref)
 
 
 @pytest.mark.parametrize("shape", [(4, 32, 112, 256), (4, 64, 56, 128)], ids=["l4", "l3"])

@@ -52,6 +52,34 @@ static hipError_t stream_ref(const void* a, const void* b, void* o, int B, int C
                       : pwc::stream::pick<float, 2, 128>(a, b, o, B, C, H, W, 0, 32.f, 0);
 }
 
+// geometries the harness can time (PWC_DEBUG strip_geo=N; the library ships 4 = GeoL4 and
+// 10 = GeoF, its default at W = 112)
+using G5 = pwc::strip::Geo<32, 12, 56, 2, 2, 2>;
+using G6 = pwc::strip::Geo<32, 12, 56, 2, 2, 1>;
+using G7 = pwc::strip::Geo<32, 12, 56, 2, 4, 1>;
+using G8 = pwc::strip::Geo<32, 12, 56, 2, 4, 2>;
+using G9 = pwc::strip::Geo<32, 6, 56, 1, 2, 2>;
+using G10 = pwc::strip::GeoF;
+static int g_geo = 10;
+template <class F>
+static auto with_geo(F&& f) {
+  switch (g_geo) {
+    case 4: return f(pwc::strip::GeoL4{});
+    case 6: return f(G6{});
+    case 7: return f(G7{});
+    case 8: return f(G8{});
+    case 9: return f(G9{});
+    case 10: return f(G10{});
+    case 5: return f(G5{});
+    default: return f(G10{});
+  }
+}
+static hipError_t strip_call(const void* a, const void* b, void* o, int B, int H, int W) {
+  return with_geo([&](auto g) {
+    return pwc::strip::launch<decltype(g)>(a, b, o, B, H, W, 32.f, 0);
+  });
+}
+
 __global__ void swap_probe(unsigned* o) {
   const unsigned l = threadIdx.x;
   const auto r = __builtin_amdgcn_permlane32_swap(l, 100 + l, false, false);
@@ -73,6 +101,7 @@ int main(int argc, char** argv) {
   const int H = argc > 3 ? std::atoi(argv[3]) : 96;
   const int W = argc > 4 ? std::atoi(argv[4]) : 112;
   const int C = 32;
+  g_geo = pwc::debug_knob("strip_geo", 10);
   {
     unsigned* d;
     CK(hipMalloc(&d, 128 * 4));
@@ -121,7 +150,7 @@ int main(int argc, char** argv) {
               NS, strip_ok ? "true" : "false");
   if (!strip_ok) return 1;
   CK(stream_ref(f1[0], f2[0], o1[0], B, C, H, W));
-  CK(pwc::corr_forward_strip(f1[0], f2[0], o2[0], B, C, H, W, 32.f, 0));
+  CK(strip_call(f1[0], f2[0], o2[0], B, H, W));
   CK(hipDeviceSynchronize());
   std::vector<float> r1(nout), r2(nout);
   CK(hipMemcpy(r1.data(), o1[0], nout * 4, hipMemcpyDeviceToHost));
@@ -193,7 +222,7 @@ int main(int argc, char** argv) {
   }
   for (int i = 0; i < 20; ++i) {
     CK(stream_ref(f1[i % NS], f2[i % NS], o1[i % NS], B, C, H, W));
-    CK(pwc::corr_forward_strip(f1[i % NS], f2[i % NS], o2[i % NS], B, C, H, W, 32.f, 0));
+    CK(strip_call(f1[i % NS], f2[i % NS], o2[i % NS], B, H, W));
   }
   CK(hipDeviceSynchronize());
   // A: stream x iters, then strip x iters (back to back within each kernel)
@@ -222,7 +251,7 @@ int main(int argc, char** argv) {
     if (warm > 0) touch(i % NS);
     pwc::g_e0 = e0[iters + i];
     pwc::g_e1 = e1[iters + i];
-    CK(pwc::corr_forward_strip(f1[i % NS], f2[i % NS], o2[i % NS], B, C, H, W, 32.f, 0));
+    CK(strip_call(f1[i % NS], f2[i % NS], o2[i % NS], B, H, W));
   }
   CK(hipDeviceSynchronize());
   double ta = 0, tb = 0;
@@ -240,57 +269,70 @@ int main(int argc, char** argv) {
   {
     // one more batch of launches with the census buffer armed: per launch, each stamp's
     // LATEST workgroup relative to the launch's earliest workgroup start, and the mean
-    // per-workgroup span from its own start (us); quad A = wave 0, quad B = wave 4
-    const int nb = B * 2 * (((H + 1) / 2 + 5) / 6) * (W / 56), CI = 50;
+    // per-workgroup span from its own start (us); quad A = wave 0, quad B = wave WPP
+    const int nb = (int)with_geo([&](auto g) {
+      return pwc::strip::grid_blocks<decltype(g)>(B, H, W);
+    });
+    const int nstep = with_geo([&](auto g) { return decltype(g)::NSTEP; }), CI = 50;
     unsigned long long* cen;
-    CK(hipMalloc(&cen, (size_t)CI * nb * 32 * 8));
-    CK(hipMemset(cen, 0, (size_t)CI * nb * 32 * 8));
+    CK(hipMalloc(&cen, (size_t)CI * nb * 64 * 8));
+    CK(hipMemset(cen, 0, (size_t)CI * nb * 64 * 8));
     for (int i = 0; i < CI; ++i) {
-      unsigned long long* p = cen + (size_t)i * nb * 32;
+      unsigned long long* p = cen + (size_t)i * nb * 64;
       CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::strip::g_census), &p, sizeof(p)));
-      CK(pwc::corr_forward_strip(f1[i % NS], f2[i % NS], o2[i % NS], B, C, H, W, 32.f, 0));
+      CK(strip_call(f1[i % NS], f2[i % NS], o2[i % NS], B, H, W));
     }
     unsigned long long* np = nullptr;
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::strip::g_census), &np, sizeof(np)));
     CK(hipDeviceSynchronize());
-    std::vector<unsigned long long> c((size_t)CI * nb * 32);
+    std::vector<unsigned long long> c((size_t)CI * nb * 64);
     CK(hipMemcpy(c.data(), cen, c.size() * 8, hipMemcpyDeviceToHost));
-    double mx[32] = {}, mean[32] = {}, skew = 0;
+    double mx[64] = {}, mean[64] = {}, skew = 0;
     for (int i = 0; i < CI; ++i) {
-      const unsigned long long* L = c.data() + (size_t)i * nb * 32;
+      const unsigned long long* L = c.data() + (size_t)i * nb * 64;
       unsigned long long t0 = ~0ull, t0max = 0;
       for (int b = 0; b < nb; ++b) {
-        t0 = std::min(t0, L[b * 32]);
-        t0max = std::max(t0max, L[b * 32]);
+        t0 = std::min(t0, L[b * 64]);
+        t0max = std::max(t0max, L[b * 64]);
       }
       skew += (t0max - t0) * 0.01;
-      for (int k = 1; k < 32; ++k) {
+      for (int k = 1; k < 64; ++k) {
         unsigned long long m = 0;
         double sm = 0;
         for (int b = 0; b < nb; ++b) {
-          m = std::max(m, L[b * 32 + k]);
-          sm += L[b * 32 + k] ? (double)(L[b * 32 + k] - L[b * 32]) : 0.0;
+          const int base = k >= 32 ? 32 : 0;  // quad B and the loader: quad B's entry stamp
+          m = std::max(m, L[b * 64 + k]);
+          sm += L[b * 64 + k] ? (double)(L[b * 64 + k] - L[b * 64 + base]) : 0.0;
         }
         mx[k] += m ? (m - t0) * 0.01 : 0.0;
         mean[k] += sm / nb * 0.01;
       }
     }
-    const char* nm[16] = {"start", "first_data", "s0_loop", "s0_reduced", "s0_stored",
-                          "s1_loop", "s1_reduced", "s1_stored", "s2_loop", "s2_reduced",
-                          "s2_stored", "", "", "ld_group0", "ld_window", "ld_all"};
-    std::printf("{\"census_start_skew_us\": %.2f", skew / CI);
-    for (int k = 1; k < 16; ++k)
-      if (nm[k][0]) std::printf(", \"%s\": [%.2f, %.2f]", nm[k], mx[k] / CI, mean[k] / CI);
+    auto name = [&](int k) -> std::string {
+      if (k == 1) return "first_data";
+      if (k >= 2 && k < 2 + 3 * nstep) {
+        const char* ph[3] = {"loop", "reduced", "stored"};
+        return "s" + std::to_string((k - 2) / 3) + "_" + ph[(k - 2) % 3];
+      }
+      return "";
+    };
+    std::printf("{\"geometry\": %d, \"census_start_skew_us\": %.2f", g_geo, skew / CI);
+    for (int k = 1; k < 32; ++k)
+      if (!name(k).empty()) std::printf(", \"%s\": [%.2f, %.2f]", name(k).c_str(), mx[k] / CI, mean[k] / CI);
+    const char* ld[3] = {"ld_group0", "ld_window", "ld_all"};
+    for (int k = 0; k < 3; ++k)
+      std::printf(", \"%s\": [%.2f, %.2f]", ld[k], mx[61 + k] / CI, mean[61 + k] / CI);
     std::printf(", \"quadB\": {");
-    for (int k = 17; k < 27; ++k)
-      std::printf("%s\"%s\": %.2f", k > 17 ? ", " : "", nm[k - 16], mean[k] / CI);
+    for (int k = 33; k < 32 + 2 + 3 * nstep; ++k)
+      std::printf("%s\"%s\": %.2f", k > 33 ? ", " : "", name(k - 32).c_str(), mean[k] / CI);
     std::printf("}}  ([latest workgroup vs earliest start, mean per-workgroup span] us)\n");
   }
 #endif
   const double bytes = (double)B * (2.0 * C * H * W + 81.0 * H * W) * 4;
-  std::printf("{\"stream_us\": %.2f, \"strip_us\": %.2f, \"strip_median_us\": %.2f, "
-              "\"strip_frac_8TBs\": %.3f, \"stream_frac_8TBs\": %.3f}\n",
-              ta / iters, tb / iters, vb[iters / 2], bytes / (tb / iters * 1e-6) / 8e12,
+  std::printf("{\"strip_geo\": %d, \"stream_us\": %.2f, \"strip_us\": %.2f, "
+              "\"strip_median_us\": %.2f, \"strip_frac_8TBs\": %.3f, \"stream_frac_8TBs\": %.3f}\n",
+              g_geo, ta / iters, tb / iters, vb[iters / 2],
+              bytes / (tb / iters * 1e-6) / 8e12,
               bytes / (ta / iters * 1e-6) / 8e12);
   return 0;
 }
