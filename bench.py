@@ -595,12 +595,19 @@ def cpu_topology():
     CPU quota (the box's share; None if unlimited), physical cores and SMT from /proc/cpuinfo."""
     info = {"host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
             "cgroup_cpus": None, "physical_cores": None, "smt": None, "cpu": cpu_model()}
-    try:
+    try:  # cgroup v2, then v1
         q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
         if q != "max":
             info["cgroup_cpus"] = round(int(q) / int(per), 2)
     except (OSError, ValueError):
-        pass
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                info["cgroup_cpus"] = round(q / per, 2)
+        except (OSError, ValueError):
+            pass
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
     try:
         cores = set()
         phys = core = None
@@ -622,44 +629,55 @@ def cpu_topology():
     return info
 
 
+def progress(msg):
+    """One line on stderr per bench phase (a long phase with no output looks hung)."""
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline_torch(shapes, batches=(8, 1), warmup=3, runs=5, max_seconds=12.0):
     """The reference's pure-PyTorch CPU path (WarpingLayer + CostVolumeLayer at l0..l4,
-    oracle/torch_ref.py) as BASELINE.md's CPU-baseline plan times it: torch.set_num_threads(
-    os.cpu_count()), B = 8 and B = 1 synthetic pairs of the 384x448 pyramid shapes, 3 warm-up
-    passes, then the median of >= 5 timed passes (more while the time budget lasts).  When the
-    process's usable CPUs (affinity, cgroup quota) are fewer than os.cpu_count(), the line is
-    also timed at that count and the faster thread count is the reported value (both listed)."""
+    oracle/torch_ref.py) as BASELINE.md's CPU-baseline plan times it: B = 8 and B = 1 synthetic
+    pairs of the 384x448 pyramid shapes, 3 warm-up passes, then the median of >= 5 timed
+    passes (more while the time budget lasts), at torch.set_num_threads(os.cpu_count()) and,
+    where fewer CPUs are usable by this process (affinity, cgroup quota), at that count too;
+    the reported value is the faster thread count's (every line is listed).  A thread count
+    whose first pass alone overruns the budget is recorded as skipped."""
     from oracle import torch_ref as T
     topo = cpu_topology()
     usable = topo["affinity_cpus"]
     if topo["cgroup_cpus"]:
         usable = max(1, min(usable, int(topo["cgroup_cpus"])))
-    counts = sorted({os.cpu_count(), usable}, reverse=True)
+    counts = sorted({usable, os.cpu_count()})  # usable first: the all-CPU line may be slow
     prev = torch.get_num_threads()
-    lines = []
+    lines, skipped = [], []
     per_budget = max_seconds / (len(counts) * len(batches))
     try:
         for thr in counts:
             torch.set_num_threads(thr)
             for B in batches:
+                progress(f"cpu baseline: {thr} threads, B={B}")
                 gen = torch.Generator().manual_seed(0)
                 data = [(torch.randn(B, C, h, w, generator=gen),
                          torch.randn(B, C, h, w, generator=gen),
                          torch.randn(B, 2, h, w, generator=gen) * 2) for (C, h, w) in shapes]
 
                 def one():
+                    t0 = time.perf_counter()
                     with torch.no_grad():
                         for x1, x2, fl in data:
                             T.cost_volume(x1, T.warp(x2, fl), SEARCH_RANGE)
+                    return time.perf_counter() - t0
 
-                for _ in range(warmup):
+                first = one()
+                if first > 4 * per_budget:
+                    skipped.append(dict(B=B, threads=thr, first_pass_s=round(first, 2)))
+                    continue
+                for _ in range(warmup - 1):
                     one()
                 times = []
                 t_end = time.perf_counter() + per_budget
                 while len(times) < runs or (time.perf_counter() < t_end and len(times) < 200):
-                    t0 = time.perf_counter()
-                    one()
-                    times.append(time.perf_counter() - t0)
+                    times.append(one())
                 med = float(np.median(times))
                 lines.append(dict(B=B, threads=thr, value=round(B / med, 2),
                                   median_ms=round(med * 1e3, 2), runs=len(times)))
@@ -667,7 +685,7 @@ def cpu_baseline_torch(shapes, batches=(8, 1), warmup=3, runs=5, max_seconds=12.
         torch.set_num_threads(prev)
     b8 = max((l for l in lines if l["B"] == max(batches)), key=lambda l: l["value"])
     return dict(value=b8["value"], unit="image-pairs/s", cores=b8["threads"], kind="port",
-                usable_cpus=usable, lines=lines, **topo,
+                usable_cpus=usable, lines=lines, skipped=skipped, **topo,
                 sample=f"B={b8['B']} synthetic pairs, median of {b8['runs']} passes after "
                        f"{warmup} warm-ups at torch.set_num_threads({b8['threads']}) (the faster "
                        f"of {counts}; every line in 'lines'): the reference's pure-PyTorch CPU "
@@ -1067,10 +1085,12 @@ def main(argv=None):
             ok = bool(flag.item())
         return ok, diff
 
+    progress(f"{args.warmup} warm-up + {args.steps} timed steps")
     elapsed, issued, per_rank = timed(step, None if cpu else evs)
     replay_ok, replay_diff = self_check(step, pass_)
     grouped = None
     if gpass is not None:
+        progress("grouped mode")
         g_el, g_issued, g_per_rank = timed(gstep, gevs)
         g_ok, g_diff = self_check(gstep, gpass)
         g_kern = float(np.mean([a.elapsed_time(b) for a, b in gevs]))
@@ -1152,6 +1172,7 @@ def main(argv=None):
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
         traffic, tsrc = None, None
         if not args.no_pmc and rank == 0 and world == 1:
+            progress("live PMC passes")
             traffic, tsrc = live_pmc_traffic(B, args.height, args.width, args.dtype)
         if traffic is None and args.dtype == "fp32" and (B, args.height, args.width) == (
                 8, 384, 448):
@@ -1172,8 +1193,10 @@ def main(argv=None):
             "avg_launch_us": round(kern_ms * 1e3, 3),
         }
     if rank == 0 and world == 1 and not cpu and not args.no_corr4:
+        progress("Corr4 line")
         result["roofline_corr4"] = corr4_roofline(dev, dtype, B, shapes[-1])
     if rank == 0 and world == 1 and not cpu and not args.no_net_forward:
+        progress("Net forward")
         result["net_forward"] = net_forward(dev, B, args.height, args.width,
                                             elapsed / args.steps * 1e3)
     if rank == 0 and world == 1 and not cpu and not args.no_cpu_baseline:
@@ -1181,8 +1204,15 @@ def main(argv=None):
                                                     max_seconds=args.cpu_seconds)
         result["cpu_baseline"]["speedup"] = round(value / result["cpu_baseline"]["value"], 1)
         thr = result["cpu_baseline"]["cores"]
+        progress(f"C port baseline ({thr} threads)")
         result["cpu_baseline_port"] = cpu_baseline_port(shapes, B, args.cpu_seconds / 2, thr)
-        result["cpu_config1"] = cpu_config1(args.cpu_seconds / 2)
+        progress("config 1 (Net forward on the CPU)")
+        prev = torch.get_num_threads()
+        torch.set_num_threads(thr)
+        try:
+            result["cpu_config1"] = cpu_config1(args.cpu_seconds / 2)
+        finally:
+            torch.set_num_threads(prev)
     ok = replay_ok and (shards is None or shards["ok"]) and (bcast is None or bcast["ok"])
     if rank == 0:
         print(json.dumps(result), flush=True)
