@@ -638,16 +638,19 @@ def cpu_baseline_torch(shapes, batches=(8, 1), warmup=3, runs=5, max_seconds=12.
     """The reference's pure-PyTorch CPU path (WarpingLayer + CostVolumeLayer at l0..l4,
     oracle/torch_ref.py) as BASELINE.md's CPU-baseline plan times it: B = 8 and B = 1 synthetic
     pairs of the 384x448 pyramid shapes, 3 warm-up passes, then the median of >= 5 timed
-    passes (more while the time budget lasts), at torch.set_num_threads(os.cpu_count()) and,
-    where fewer CPUs are usable by this process (affinity, cgroup quota), at that count too;
-    the reported value is the faster thread count's (every line is listed).  A thread count
-    whose first pass alone overruns the budget is recorded as skipped."""
+    passes (more while the time budget lasts), at torch.set_num_threads(usable CPUs):
+    os.cpu_count() unless an affinity mask or a cgroup CPU quota gives this process fewer
+    (both are reported).  A line whose first pass alone overruns the budget is recorded as
+    skipped."""
     from oracle import torch_ref as T
     topo = cpu_topology()
     usable = topo["affinity_cpus"]
     if topo["cgroup_cpus"]:
         usable = max(1, min(usable, int(topo["cgroup_cpus"])))
-    counts = sorted({usable, os.cpu_count()})  # usable first: the all-CPU line may be slow
+    # os.cpu_count() when this process may use every CPU; under an affinity mask or a cgroup
+    # CPU quota (the GPU box: 16 of 256 host CPUs) the usable count -- more threads than the
+    # quota only queue (one 256-thread pass under a 16-CPU quota took 60-120 s)
+    counts = [usable]
     prev = torch.get_num_threads()
     lines, skipped = [], []
     per_budget = max_seconds / (len(counts) * len(batches))
@@ -687,8 +690,9 @@ def cpu_baseline_torch(shapes, batches=(8, 1), warmup=3, runs=5, max_seconds=12.
     return dict(value=b8["value"], unit="image-pairs/s", cores=b8["threads"], kind="port",
                 usable_cpus=usable, lines=lines, skipped=skipped, **topo,
                 sample=f"B={b8['B']} synthetic pairs, median of {b8['runs']} passes after "
-                       f"{warmup} warm-ups at torch.set_num_threads({b8['threads']}) (the faster "
-                       f"of {counts}; every line in 'lines'): the reference's pure-PyTorch CPU "
+                       f"{warmup} warm-ups at torch.set_num_threads({b8['threads']}) (the CPUs "
+                       f"this process may use of the host's {os.cpu_count()}; B=1 in 'lines'): "
+                       "the reference's pure-PyTorch CPU "
                        "path (WarpingLayer = grid_sample(align_corners=True) + "
                        "CostVolumeLayer(sr=4), modules.py:31-74) at l0-l4 of 384x448, fp32. "
                        "NOTE: the correlation timed here is CostVolumeLayer(sr=4) (the "

@@ -87,6 +87,18 @@ __global__ void swap_probe(unsigned* o) {
   o[64 + l] = r[1];
 }
 
+// STRIP_PRODUCER: rewrite f2 (nontemporal 16-B stores, as the warp kernel writes x2_warp)
+// right before each timed strip launch -- the bench step's order (warp, then correlation)
+// (STRIP_PRODUCER=1 nt, 2 plain, 3 sc1, 4 sc0 sc1: the store cache policy of the producer)
+typedef float pf4 __attribute__((ext_vector_type(4)));
+template <int AUX>
+__global__ void produce(const pf4* __restrict__ src, pf4* __restrict__ dst, unsigned n) {
+  const unsigned i = blockIdx.x * 256 + threadIdx.x;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, (int)(n * 16), 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(src[i < n ? i : 0], r, (int)(i < n ? i * 16 : 0x80000000u), 0, AUX);
+}
+
 // one dword per `stride` bytes of a buffer (STRIP_WARM); the sum goes to a sink so the loads stay
 __global__ void touch_pages(const char* p, unsigned n, unsigned stride, unsigned* sink) {
   const unsigned i = blockIdx.x * 256 + threadIdx.x;
@@ -247,8 +259,25 @@ int main(int argc, char** argv) {
                          reinterpret_cast<const char*>(bufs[j]), n, (unsigned)warm, sink);
     }
   };
+  const char* prod_env = std::getenv("STRIP_PRODUCER");
+  const int prod = prod_env ? std::atoi(prod_env) : 0;
+  float* psrc = nullptr;
+  if (prod) {
+    CK(hipMalloc(&psrc, nin * 4));
+    CK(hipMemcpy(psrc, h2.data(), nin * 4, hipMemcpyHostToDevice));
+  }
   for (int i = 0; i < iters; ++i) {
     if (warm > 0) touch(i % NS);
+    if (prod) {
+      const dim3 g((unsigned)((nin / 4 + 255) / 256));
+      const pf4* a = (const pf4*)psrc;
+      pf4* d = (pf4*)f2[i % NS];
+      const unsigned n4 = (unsigned)(nin / 4);
+      if (prod == 2) hipLaunchKernelGGL(produce<0>, g, dim3(256), 0, 0, a, d, n4);
+      else if (prod == 3) hipLaunchKernelGGL(produce<16>, g, dim3(256), 0, 0, a, d, n4);
+      else if (prod == 4) hipLaunchKernelGGL(produce<17>, g, dim3(256), 0, 0, a, d, n4);
+      else hipLaunchKernelGGL(produce<2>, g, dim3(256), 0, 0, a, d, n4);
+    }
     pwc::g_e0 = e0[iters + i];
     pwc::g_e1 = e1[iters + i];
     CK(strip_call(f1[i % NS], f2[i % NS], o2[i % NS], B, H, W));
