@@ -519,6 +519,7 @@ hipError_t corr_forward_stream(const void*, const void*, void*, int, int, int, i
 bool corr_stream_accepts(const void*, const void*, const void*, int, int, int, int, int, int);
 bool corr_mstrip16_accepts(const void*, const void*, const void*, int, int, int, int, int, int,
                            int);
+bool corr_strip_accepts(const void*, const void*, const void*, int, int, int, int, int, int, int);
 bool corr_rows_accepts(int, int, int, int, int);
 bool warp_corr_band_accepts(int, int, int, int, int);
 
@@ -534,7 +535,8 @@ int corr_forward_path(const void* in1, const void* in2, const void* out, int B, 
   // matrix-core strip takes go there even where the stream kernel itself would decline
   if ((dtype == 0 || half) && pad == md && md / s2 == 4 && (s2 == 1 || s2 == 2) &&
       (corr_stream_accepts(in1, in2, out, B, C, H, W, s2, half ? 1 : 0) ||
-       corr_mstrip16_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)))
+       corr_mstrip16_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout) ||
+       corr_strip_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)))
     return kPathStream;
   const bool c9 = layout == kRaster && s2 == 2 && pad == md && (md == 8 || md == 9);
   if (c9 && dtype == 0 && band_enabled() && (H + 1) / 2 <= 6 &&

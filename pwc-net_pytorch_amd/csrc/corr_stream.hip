@@ -778,13 +778,13 @@ hipError_t corr_forward_stream(const void* in1, const void* in2, void* out, int 
     const hipError_t e = corr_forward_mstrip16(in1, in2, out, B, C, H, W, divisor, stream);
     if (e != hipErrorNotSupported) return e;
   }
-  if (!corr_stream_accepts(in1, in2, out, B, C, H, W, s2, dtype)) return hipErrorNotSupported;
-  // fp32 model-config grids of C = 32 (config 2 l4): the strip kernel (corr_strip.hip), whose
-  // stores drain under compute; it declines what it does not serve
+  // fp32 model-config grids of C = 32 (config 2 l4) and C = 64 at W = 56 (config 2 l3): the
+  // strip kernel (corr_strip.hip), also where the stream kernel would decline the grid
   if (corr_strip_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)) {
     const hipError_t e = corr_forward_strip(in1, in2, out, B, C, H, W, divisor, stream);
     if (e != hipErrorNotSupported) return e;
   }
+  if (!corr_stream_accepts(in1, in2, out, B, C, H, W, s2, dtype)) return hipErrorNotSupported;
   const int twp = (W % 112 == 0 || W < 112) ? 112 : 128;  // column tile width in pixels
   using namespace stream;
 #define PWC_PICK(T)                                                                            \

@@ -553,37 +553,61 @@ using GeoL4 = Geo<32, 6, 56>;
 // stores alone, tools/store_probe.hip); 6 parity rows, the (tj, segment) tasks of a row split
 // over two workgroups (10 staged f2 rows each)
 using GeoF = Geo<32, 6, 112, 2, 2, 1, true>;
+// C = 64, W = 56 (config 2 l3): the same whole-row form, 3 parity rows per workgroup (7 staged
+// f2 rows, 112 KB), one step of six compute waves
+using GeoF3 = Geo<64, 3, 56, 2, 3, 1, true>;
 
 }  // namespace strip
 
-// Whether the strip kernel serves this problem: fp32, model.py:24's stride-2 displacements in
-// raster order (dr = 4, pad = md, k = 1, s1 = 1: checked by the caller), C = 32, W a multiple
-// of the 56-px strip, 16-B aligned buffers, an output the kernel's 32-bit buffer addressing
-// reaches, the max(v, slope v) epilogue, and at least about one workgroup per CU (smaller grids
-// leave CUs idle: the stream kernel's 3-row bands suit them better).  Knob strip=0 disables it
-// (measurement of the stream kernel); strip_geo=4 selects the 56-px strips at W = 112.
-bool corr_strip_accepts(const void* in1, const void* in2, const void* out, int B, int C, int H,
-                        int W, int s2, int dtype, int layout) {
-  using G = strip::GeoL4;
-  if (dtype != 0 || s2 != 2 || layout != kRaster || C != G::C) return false;
-  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16) return false;
-  if (W % G::TW || H < 2 || (size_t)C * H * W * 4 >= 0x7ffffff0ull) return false;
+// Which strip geometry serves this problem (0: none): fp32, model.py:24's stride-2 displacements
+// in raster order (dr = 4, pad = md, k = 1, s1 = 1: checked by the caller), 16-B aligned
+// buffers, an output the kernel's 32-bit buffer addressing reaches, the max(v, slope v)
+// epilogue, and at least about one workgroup per CU (smaller grids leave CUs idle: the stream
+// and row-band kernels suit them better); C = 32 at W = 112 (whole rows) or a multiple of
+// 56 (strips), C = 64 at W = 56 (whole rows).  Knobs: strip=0 disables the kernel
+// (measurement of the stream / row-band kernels), strip_geo=4 selects the 56-px strips at
+// W = 112, strip_l3=0 leaves C = 64 to the row-band kernel.
+enum StripPlan : int { kStripNone = 0, kStripL4 = 1, kStripF = 2, kStripF3 = 3 };
+static int strip_plan(const void* in1, const void* in2, const void* out, int B, int C, int H,
+                      int W, int s2, int dtype, int layout) {
+  if (dtype != 0 || s2 != 2 || layout != kRaster) return kStripNone;
+  if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16) return kStripNone;
+  if (H < 2 || (size_t)C * H * W * 4 >= 0x7ffffff0ull) return kStripNone;
   // the 81-plane output is addressed through one 32-bit buffer resource whose out-of-range
   // sentinel is 2^31: it must stay below that (larger grids go to the size_t stream kernel)
-  if ((size_t)81 * H * W * 4 >= 0x7ffffff0ull) return false;
-  if (!(current_epi().slope <= 1.f)) return false;  // the max(v, slope v) epilogue
-  if (debug_knob("strip", 1) == 0) return false;
-  return strip::grid_blocks<G>(B, H, W) >= 192;
+  if ((size_t)81 * H * W * 4 >= 0x7ffffff0ull) return kStripNone;
+  if (!(current_epi().slope <= 1.f)) return kStripNone;  // the max(v, slope v) epilogue
+  if (debug_knob("strip", 1) == 0) return kStripNone;
+  if (C == 32) {
+    if (W == strip::GeoF::TW && debug_knob("strip_geo", 5) != 4 &&
+        strip::grid_blocks<strip::GeoF>(B, H, W) >= 192)
+      return kStripF;
+    if (W % strip::GeoL4::TW == 0 && strip::grid_blocks<strip::GeoL4>(B, H, W) >= 192)
+      return kStripL4;
+  }
+  if (C == 64 && W == strip::GeoF3::TW && debug_knob("strip_l3", 1) != 0 &&
+      strip::grid_blocks<strip::GeoF3>(B, H, W) >= 192)
+    return kStripF3;
+  return kStripNone;
+}
+
+bool corr_strip_accepts(const void* in1, const void* in2, const void* out, int B, int C, int H,
+                        int W, int s2, int dtype, int layout) {
+  return strip_plan(in1, in2, out, B, C, H, W, s2, dtype, layout) != kStripNone;
 }
 
 hipError_t corr_forward_strip(const void* in1, const void* in2, void* out, int B, int C, int H,
                               int W, float divisor, hipStream_t stream) {
-  if (!corr_strip_accepts(in1, in2, out, B, C, H, W, 2, 0, kRaster)) return hipErrorNotSupported;
-  // whole rows where the width is the full-row geometry's (knob strip_geo=4: the 56-px strips)
-  if (W == strip::GeoF::TW && debug_knob("strip_geo", 5) != 4 &&
-      strip::grid_blocks<strip::GeoF>(B, H, W) >= 192)
-    return strip::launch<strip::GeoF>(in1, in2, out, B, H, W, divisor, stream);
-  return strip::launch<strip::GeoL4>(in1, in2, out, B, H, W, divisor, stream);
+  switch (strip_plan(in1, in2, out, B, C, H, W, 2, 0, kRaster)) {
+    case kStripF:
+      return strip::launch<strip::GeoF>(in1, in2, out, B, H, W, divisor, stream);
+    case kStripF3:
+      return strip::launch<strip::GeoF3>(in1, in2, out, B, H, W, divisor, stream);
+    case kStripL4:
+      return strip::launch<strip::GeoL4>(in1, in2, out, B, H, W, divisor, stream);
+    default:
+      return hipErrorNotSupported;
+  }
 }
 
 }  // namespace pwc

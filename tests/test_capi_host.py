@@ -227,7 +227,7 @@ def test_corr_forward_plan_routes_and_declines():
     plan = _lib.corr_forward_plan
     c9 = (9, 1, 9, 1, 2)
     assert plan(8, 32, 96, 112, *c9) == "strip"                # config 2 l4
-    assert plan(8, 64, 48, 56, *c9) == "rows"                  # config 2 l3
+    assert plan(8, 64, 48, 56, *c9) == "strip"                 # config 2 l3 (C = 64 rows)
     assert plan(8, 96, 24, 28, *c9) == "rows"                  # config 2 l2
     assert plan(8, 192, 6, 7, *c9) == "band"                   # config 2 l0
     assert plan(16, 32, 112, 256, *c9, dtype=1) == "mstrip16"  # config 4 l4

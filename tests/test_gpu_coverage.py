@@ -75,6 +75,12 @@ FWD = [
     ("corr9", torch.float32, (8, 32, 90, 112), "strip full rows, partial row group"),
     ("corr9", torch.float32, (8, 32, 95, 112), "strip full rows, odd height"),
     ("corr9", torch.float32, (4, 32, 192, 224), "strip, 4 strips per row"),
+    # its C = 64 whole-row geometry at W = 56 (GeoF3, config 2 l3): the shape, the smallest
+    # batch, a partial last row group (H = 46: 23 parity rows in groups of 3), an odd height
+    ("corr9", torch.float32, (8, 64, 48, 56), "strip C=64 whole rows (config 2 l3)"),
+    ("corr9", torch.float32, (6, 64, 48, 56), "strip C=64, B=6"),
+    ("corr9", torch.float32, (8, 64, 46, 56), "strip C=64, partial row group"),
+    ("corr9", torch.float32, (8, 64, 47, 56), "strip C=64, odd height"),
     # the matrix-core fp16 strip kernel (corr_mstrip16.hip): its smallest batch at Sintel l4, a
     # partial last chunk (50 parity rows in chunks of 14) with a partial last strip (W = 200),
     # and an odd height (parity rows 50 / 49)
@@ -135,6 +141,32 @@ def test_cost_volume_448x1024_b4(shape):
     out = cost_volume_forward(a, b, 4)
     torch.cuda.synchronize()
     _check(out, O.cvl_forward(an, bn, 4), torch.float32)
+
+
+def test_strip_c64_into_cat_slice_leaky():
+    """model.py:83-84 + :89/91 at config 2's l3 (C = 64, 48 x 56, B = 8) through the strip
+    kernel's C = 64 whole-row geometry: the cat slice with leaky_relu(0.01) fused, and equal bit
+    for bit to the row-band kernel's volume (knob strip_l3=0) before the activation."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_forward, corr_forward_into
+    B, C, H, W = 8, 64, 48, 56
+    a, an = _rand((B, C, H, W), torch.float32, "l3a")
+    b, bn = _rand((B, C, H, W), torch.float32, "l3b")
+    cat = torch.full((B, C + 81 + 2, H, W), 7.0, device=DEV)
+    corr_forward_into(a, b, cat[:, C:C + 81], 9, 1, 9, 1, 2, negative_slope=0.01)
+    plain = corr_forward(a, b, 9, 1, 9, 1, 2)
+    _lib.set_debug("strip_l3=0")
+    try:
+        rows = corr_forward(a, b, 9, 1, 9, 1, 2)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_debug("")
+    ref = O.corr_forward(an, bn, 9, 1, 9, 1, 2)
+    np.testing.assert_allclose(_np(plain), ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_np(rows), ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_np(cat[:, C:C + 81]), np.where(ref > 0, ref, ref * 0.01),
+                               rtol=1e-5, atol=1e-5)
+    assert bool((cat[:, :C] == 7.0).all()) and bool((cat[:, C + 81:] == 7.0).all())
 
 
 def test_strip_into_cat_slice_leaky():

@@ -113,6 +113,25 @@ __global__ __launch_bounds__(512) void parity_full_pattern(float* out, int gap) 
   }
 }
 
+// generic shapes (the coarse levels): nwg workgroups each write a block of 81 planes x rows;
+// PAR: a workgroup's rows are one row parity (rows 2r + p), else consecutive image rows
+template <bool PAR>
+__global__ __launch_bounds__(512) void level_pattern(float* out, int Hh, int Ww, int rows_per) {
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bands = (PAR ? (Hh / 2) : Hh) / rows_per;
+  const int b = t % bands, rest = t / bands;
+  const int p = PAR ? rest % 2 : 0, n = PAR ? rest / 2 : rest;
+  const unsigned plane = (unsigned)(Hh * Ww) * 4u, img = 81u * plane;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(out + (size_t)n * img / 4, (short)0, (int)img, 0x00020000);
+  const int qpr = Ww / 4, nq = 81 * rows_per * qpr;
+  for (int k = threadIdx.x; k < nq; k += 512) {
+    const int pl = k / (rows_per * qpr), rem = k % (rows_per * qpr), rr = rem / qpr, xq = rem % qpr;
+    const int y = PAR ? 2 * (b * rows_per + rr) + p : b * rows_per + rr;
+    st16<2>(r, (unsigned)((pl * Hh + y) * Ww) * 4u + xq * 16u, u32x4{1u, 2u, 3u, (unsigned)k});
+  }
+}
+
 __global__ __launch_bounds__(512) void flat_pattern(float* out, int gap) {
   const unsigned total_q = (unsigned)B * IMG / 16;
   const unsigned per = (total_q + 255) / 256;
@@ -164,5 +183,32 @@ int main() {
   if (run("parity_full_nt", parity_full_pattern<2>, 0)) return 1;
   if (run("parity_full_plain", parity_full_pattern<0>, 0)) return 1;
   if (run("flat_nt", flat_pattern, 0)) return 1;
+  // coarse levels, B = 8: l3 (48 x 56), l2 (24 x 28); parity bands vs consecutive rows
+  auto runl = [&](const char* name, auto kern, int Hh, int Ww, int rows_per, int nwg) -> int {
+    const double mb = 8.0 * 81 * Hh * Ww * 4 / 1e6;
+    for (int i = 0; i < 20; ++i)
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), 0, 0, O[i % NS], Hh, Ww, rows_per);
+    CK(hipDeviceSynchronize());
+    for (int i = 0; i < 200; ++i)
+      hipExtLaunchKernelGGL(kern, dim3(nwg), dim3(512), 0, 0, e0[i], e1[i], 0, O[i % NS], Hh, Ww,
+                            rows_per);
+    CK(hipDeviceSynchronize());
+    double sum = 0;
+    for (int i = 0; i < 200; ++i) {
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0[i], e1[i]));
+      sum += ms;
+    }
+    const double us = sum / 200 * 1e3;
+    std::printf("{\"pattern\": \"%s\", \"us\": %.2f, \"MB\": %.1f, \"TBs\": %.3f}\n", name, us, mb,
+                mb / us);
+    return 0;
+  };
+  if (runl("l3_parity_bands_3", level_pattern<true>, 48, 56, 3, 8 * 2 * 8)) return 1;
+  if (runl("l3_rows_6", level_pattern<false>, 48, 56, 6, 8 * 8)) return 1;
+  if (runl("l3_rows_3", level_pattern<false>, 48, 56, 3, 8 * 16)) return 1;
+  if (runl("l2_parity_bands_1", level_pattern<true>, 24, 28, 1, 8 * 2 * 12)) return 1;
+  if (runl("l2_rows_2", level_pattern<false>, 24, 28, 2, 8 * 12)) return 1;
+  if (runl("l2_rows_1", level_pattern<false>, 24, 28, 1, 8 * 24)) return 1;
   return 0;
 }
