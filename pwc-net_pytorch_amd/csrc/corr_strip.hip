@@ -93,6 +93,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef PWC_STRIP_STORE_AUX  // output store cache policy (measurement builds may override)
 #define PWC_STRIP_STORE_AUX 2  // nontemporal
 #endif
+#ifndef PWC_STRIP_LAST_AUX  // the last step's stores
+#define PWC_STRIP_LAST_AUX PWC_STRIP_STORE_AUX
+#endif
 
 // C channels, R output parity rows per workgroup, TW-px column strips; the 9 x NSEG (tj, 4-px
 // segment) tasks of an output row split over TS workgroups (each stages only the f2 rows its tj
@@ -172,10 +175,14 @@ constexpr int dma_target(int j) {
   return (j > 0 ? dma_need<G>(j - 1) : 0) + 63 < G::NDMA ? (j > 0 ? dma_need<G>(j - 1) : 0) + 63
                                                          : G::NDMA;
 }
-// DMA group that completes channel pair k (LDS channel rows 2k, 2k+1)
+// DMA group that completes channel pair k (LDS channel rows 2k, 2k+1) including what its
+// reads touch: with FULL rows, channel row 2k+1's right halo is the next channel row's 2-quad
+// left pad, which can open the next DMA group (the last pair's is the ZQ quads, written at
+// kernel start)
 template <class G>
 constexpr int pair_group(int k) {
-  return ((2 * k + 2) * G::QR - 1) / 64;
+  const int g = ((2 * k + 2) * G::QR + (G::FULL ? 2 : 0) - 1) / 64;
+  return g < G::IPR - 1 ? g : G::IPR - 1;
 }
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -486,8 +493,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
       const bool ok = !(PWC_STRIP_ABL & 1) && wr && (q < 4 || chalf == 0);
       // nontemporal (aux 2): measured against sc1, nt sc1 and plain stores, 14.2 against
       // 17.0-19.9 us back to back (profiles/r04a_strip_store_policy.txt)
+      // the last step's stores with PWC_STRIP_LAST_AUX (measurement builds)
       __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0,
-                                             PWC_STRIP_STORE_AUX);
+                                             PF ? PWC_STRIP_STORE_AUX : PWC_STRIP_LAST_AUX);
     }
     CSTAMP(4 + 3 * st);  // stores issued
   };

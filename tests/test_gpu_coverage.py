@@ -143,6 +143,30 @@ def test_cost_volume_448x1024_b4(shape):
     _check(out, O.cvl_forward(an, bn, 4), torch.float32)
 
 
+@pytest.mark.parametrize("shape,knob", [((8, 64, 48, 56), "strip_l3=0"),
+                                        ((8, 32, 96, 112), "strip_geo=4")], ids=["l3", "l4"])
+def test_strip_full_rows_after_other_kernels(shape, knob):
+    """The whole-row strip geometries read each channel row's right halo from the next channel
+    row's zero pad: a read issued before that pad's DMA group landed returns whatever LDS held
+    (a round-5 bug at C = 64, caught only with other kernels' data left in LDS).  Each round
+    runs the reference-path kernel (knob) on unrelated data first, then the default on fresh
+    inputs, against the oracle."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_forward
+    for it in range(4):
+        z, _ = _rand(shape, torch.float32, "junk", it, shape, scale=50.0)
+        _lib.set_debug(knob)
+        try:
+            corr_forward(z, z, 9, 1, 9, 1, 2)
+        finally:
+            _lib.set_debug("")
+        a, an = _rand(shape, torch.float32, "sa", it, shape)
+        b, bn = _rand(shape, torch.float32, "sb", it, shape)
+        out = corr_forward(a, b, 9, 1, 9, 1, 2)
+        torch.cuda.synchronize()
+        _check(out, O.corr_forward(an, bn, 9, 1, 9, 1, 2), torch.float32)
+
+
 def test_strip_c64_into_cat_slice_leaky():
     """model.py:83-84 + :89/91 at config 2's l3 (C = 64, 48 x 56, B = 8) through the strip
     kernel's C = 64 whole-row geometry: the cat slice with leaky_relu(0.01) fused, and equal bit
