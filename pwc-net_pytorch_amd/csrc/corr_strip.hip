@@ -102,15 +102,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // meet); NQD output rows per step (two compute waves each); LA channels of LDS read-ahead.
 // FULL: the strip is the whole image row (TW == W); a channel row then stages only its 2-quad
 // left halo (zeros) before its data, and its right halo is the next channel row's left halo,
-// so a row of all channels is 2 quads per channel shorter (+ 2 zero quads after the last).
-template <int C_, int R_, int TW_, int TS_ = 1, int NQD_ = 2, int LA_ = 1, bool FULL_ = false>
+// so a row of all channels is 2 quads per channel shorter (+ 2 zero quads after the last); a
+// channel row may carry extra zero quads on the right so that a staged row is whole DMAs.
+// NCS: the channels of a task split over NCS lanes (2: halves in lanes l, l + 32; 4: quarters
+// in the four 16-lane rows), summed by permlane swaps before the stores.
+template <int C_, int R_, int TW_, int TS_ = 1, int NQD_ = 2, int LA_ = 1, bool FULL_ = false,
+          int NCS_ = 2>
 struct Geo {
-  static constexpr int C = C_, R = R_, TW = TW_, TS = TS_, NQD = NQD_, LA = LA_;
+  static constexpr int C = C_, R = R_, TW = TW_, TS = TS_, NQD = NQD_, LA = LA_, NCS = NCS_;
   static constexpr bool FULL = FULL_;
-  static constexpr int CH = C / 2;          // channels per lane half
+  static constexpr int CH = C / NCS;        // channels per lane
+  static constexpr int S = 64 / NCS;        // task slots per wave
   static constexpr int NSEG = TW / 4;       // 4-px segments per strip row
+  static constexpr int qr_full() {
+    int q = TW / 4 + 2;
+    while ((C * q) % 64) ++q;
+    return q;
+  }
   // quads per staged channel row: 8-px halo each side (shared between channel rows if FULL)
-  static constexpr int QR = FULL ? TW / 4 + 2 : (TW + 16) / 4;
+  static constexpr int QR = FULL ? qr_full() : (TW + 16) / 4;
   static constexpr int ROWQ = C * QR;       // quads per staged f2 row (all channels), DMA'd
   static constexpr int IPR = ROWQ / 64;     // LDS-DMAs per f2 row
   static constexpr int ZQ = FULL ? 2 : 0;   // zero quads after the DMA'd row (the last right halo)
@@ -131,7 +141,7 @@ struct Geo {
   static constexpr int NROW = R + TJS - 1;  // f2 parity rows of the strip
   static constexpr int NSTEP = R / NQD;
   static constexpr int WIN = NQD + TJS - 1;  // f2 rows of step 0
-  static constexpr int WPP = (NTASK + 31) / 32;  // waves per output row (32 task slots each)
+  static constexpr int WPP = (NTASK + S - 1) / S;  // waves per output row (S task slots each)
   static constexpr int NWC = WPP * NQD;     // compute waves
   static constexpr int THREADS = 64 * (NWC + 1);
   static constexpr int LDS_BYTES = NROW * SIGMA * 16;
@@ -142,14 +152,15 @@ struct Geo {
 #endif
   static constexpr int NDMA = NROW * IPR;
   static constexpr int NBAR = IPR + NSTEP - 1;  // barriers every wave executes
-  static_assert(C % 2 == 0 && TW % 4 == 0 && R % NQD == 0, "geometry");
+  static_assert((NCS == 2 || NCS == 4) && C % NCS == 0 && TW % 4 == 0 && R % NQD == 0,
+                "geometry");
   static_assert(NTASK_ALL % TS == 0, "task groups");
   static_assert(ROWQ % 64 == 0, "a staged row is whole DMAs");
   static_assert(LDS_ALLOC <= 160 * 1024 && THREADS <= 1024, "workgroup resources");
   static_assert(LA >= 1 && LA <= 2 && CH > LA, "read-ahead");
   // every read offset inside a step is an instruction immediate (16-bit); the step's row base
   // is in the address register
-  static_assert(((C - 2) * QR + 4) * 16 < 65536, "ds offsets");
+  static_assert(((C - 1) * QR + 4) * 16 < 65536, "ds offsets");
 };
 
 // Loader DMA d -> (f2 row m, DMA i of the row): step 0's rows group-major (group i of all
@@ -181,7 +192,7 @@ constexpr int dma_target(int j) {
 // kernel start)
 template <class G>
 constexpr int pair_group(int k) {
-  const int g = ((2 * k + 2) * G::QR + (G::FULL ? 2 : 0) - 1) / 64;
+  const int g = (G::NCS * (k + 1) * G::QR + (G::FULL ? 2 : 0) - 1) / 64;
   return g < G::IPR - 1 ? g : G::IPR - 1;
 }
 
@@ -292,6 +303,19 @@ __device__ __forceinline__ void swap32x4(float& a0, float& b0, float& a1, float&
       : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3));
 }
 
+// Four v_permlane16_swap_b32 (a's odd 16-lane rows <-> b's even rows), hazards as above.
+__device__ __forceinline__ void swap16x4(float& a0, float& b0, float& a1, float& b1, float& a2,
+                                         float& b2, float& a3, float& b3) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_permlane16_swap_b32 %0, %1\n\t"
+      "v_permlane16_swap_b32 %2, %3\n\t"
+      "v_permlane16_swap_b32 %4, %5\n\t"
+      "v_permlane16_swap_b32 %6, %7\n\t"
+      "s_nop 1"
+      : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3));
+}
+
 struct LaneCtx {
   uint32_t addr;                   // LDS byte address of (step-0 row qd + tj - tj_lo, channel half, segment)
   __amdgpu_buffer_rsrc_t rs1;      // f1 of this image
@@ -326,7 +350,7 @@ template <class G, bool FIRST, int K>
 __device__ __forceinline__ void issue_read(uint32_t a, f32x4 (&w)[G::LA + 1][5]) {
   if constexpr (FIRST && K > 0 && pair_group<G>(K) > pair_group<G>(K - 1))
     __builtin_amdgcn_s_barrier();
-  read5<2 * K * G::QR * 16>(a, wbuf<G, K>(w));
+  read5<G::NCS * K * G::QR * 16>(a, wbuf<G, K>(w));
 }
 
 // Channel k of a step (FIRST: step 0, whose window lands group by group; PF: the next step's
@@ -354,7 +378,7 @@ __device__ __forceinline__ void channel(const LaneCtx& lc, uint32_t f1v, uint32_
 template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
-    int H, int W, int ngrp, int ntx, float inv_divisor, OutEpi epi) {
+    int H, int W, int ngrp, int ntx, float inv_divisor, float divisor, OutEpi epi) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // logical block = (n, row parity, row group, strip, task group), task group fastest: the
   // workgroups of one image parity are neighbours and xcd_remap keeps neighbours on one XCD
@@ -385,7 +409,8 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
     for (int i = 0; i < G::IPR; ++i) {
       const int qq = 64 * i + lane;            // quad of the staged row
       const int l = qq / G::QR, qx = qq % G::QR;  // LDS channel row, quad in it
-      const int c = (l >> 1) + G::CH * (l & 1);   // channel pairs (c, c + C/2) adjacent
+      // channel k of every lane part adjacent: (k, k + CH, ...)
+      const int c = l / G::NCS + G::CH * (l % G::NCS);
       const int px = x0 - 8 + 4 * qx;
       rel[i] = px >= 0 && px < W ? ((uint32_t)c * plane_b + (uint32_t)px * 4u) : kOOB;
     }
@@ -401,8 +426,8 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
 
   // ---------------- compute waves ----------------
   const int qd = wave / G::WPP, wq = wave % G::WPP;
-  const int slot = lane & 31, chalf = lane >> 5;
-  const int gtask = 32 * wq + slot;               // task of this workgroup's group
+  const int slot = lane % G::S, chalf = lane / G::S;  // task slot, channel part
+  const int gtask = G::S * wq + slot;             // task of this workgroup's group
   const bool active = gtask < G::NTASK;
   const int tt = tg * G::NTASK + (active ? gtask : G::NTASK - 1);  // idle slots duplicate a lane
   const int tj = tt / G::NSEG, seg = tt % G::NSEG;
@@ -461,40 +486,72 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
     if constexpr (G::LA > 1) issue_read<G, FIRST, 1>(a, w);
     channel<G, FIRST, PF, 0>(lc, f1_voff<G>(lc, st + 1), a, acc, f1, w);
     CSTAMP(2 + 3 * st);  // loop done
-    // channel halves: lane l (c < C/2) and l + 32 (c >= C/2) hold partial sums of the same
-    // task.  One v_permlane32_swap per pair (ti, ti + 5) leaves both halves of the pair in
-    // each lane; their sum is displacement ti's total in one half and ti + 5's in the other.
-    float res[5][4];
+    // channel parts: lanes l + S j (j < NCS) hold partial sums of the same task; permlane
+    // swaps pair a register holding plane P in every lane with one holding plane Q: the lanes
+    // of the lower half keep P's total, the upper half Q's.  Halves (NCS 2): pairs (ti, ti + 5),
+    // the low half keeps ti 0-4, the high half 5-8.  Quarters (NCS 4): permlane32 pairs
+    // (0,2) (1,3) (4,6) (5,7) (8,8), then permlane16 pairs: part j keeps planes j, 4 + j
+    // (and part 0 plane 8).
+    constexpr int NQ = G::NCS == 2 ? 5 : 3;  // stores per lane
+    float res[NQ][4];
+    int pl[NQ];  // displacement column ti of each store
+    if constexpr (G::NCS == 2) {
 #pragma unroll
-    for (int ti = 0; ti < 5; ++ti) {
-      float x[4], y[4];
+      for (int ti = 0; ti < 5; ++ti) {
+        float x[4], y[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = acc[ti][e], y[e] = ti < 4 ? acc[ti + 5][e] : acc[ti][e];
-      swap32x4(x[0], y[0], x[1], y[1], x[2], y[2], x[3], y[3]);
+        for (int e = 0; e < 4; ++e)
+          x[e] = acc[ti][e], y[e] = ti < 4 ? acc[ti + 5][e] : acc[ti][e];
+        swap32x4(x[0], y[0], x[1], y[1], x[2], y[2], x[3], y[3]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) res[ti][e] = x[e] + y[e];
+        for (int e = 0; e < 4; ++e) res[ti][e] = x[e] + y[e];
+        pl[ti] = ti + 5 * chalf;
+      }
+    } else {
+      constexpr int PA[5] = {0, 1, 4, 5, 8}, PB[5] = {2, 3, 6, 7, 8};
+      float r1[5][4];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        float x[4], y[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = acc[PA[i]][e], y[e] = acc[PB[i]][e];
+        swap32x4(x[0], y[0], x[1], y[1], x[2], y[2], x[3], y[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r1[i][e] = x[e] + y[e];
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        float x[4], y[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = r1[2 * i][e], y[e] = i < 2 ? r1[2 * i + 1][e] : r1[4][e];
+        swap16x4(x[0], y[0], x[1], y[1], x[2], y[2], x[3], y[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) res[i][e] = x[e] + y[e];
+      }
+      pl[0] = chalf, pl[1] = 4 + chalf, pl[2] = 8;
     }
-    CSTAMP(3 + 3 * st);  // channel halves reduced
+    CSTAMP(3 + 3 * st);  // channel parts reduced
     const int yrow = yrow0 + 2 * G::NQD * st;
     const bool wr = active && px < W && st < lc.nstep_ok;
-    // the swap pairs (ti, ti + 5): the low half keeps ti, the high half ti + 5
-    const uint32_t o0 = (uint32_t)(((tj * 9 + 5 * chalf) * H + yrow) * W + px) * 4u;
-    const uint32_t ostep = plane_b;  // next displacement plane
+    const uint32_t o0 = (uint32_t)(((tj * 9) * H + yrow) * W + px) * 4u;
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       u32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float o = res[q][e] * inv_divisor;  // exact: the divisor is a power of two
+        // exact 2^-k multiply, or the reference's fp32 division (cu:98-100) when C is not a
+        // power of two (C = 96)
+        const float o = inv_divisor != 0.f ? res[q][e] * inv_divisor : res[q][e] / divisor;
         v[e] = __builtin_bit_cast(uint32_t, fmaxf(o, o * slope));
       }
       // measurement builds (tools/strip_bench, -DPWC_STRIP_ABL=mask): 1 = stores discarded
-      const bool ok = !(PWC_STRIP_ABL & 1) && wr && (q < 4 || chalf == 0);
+      const bool keep = G::NCS == 2 ? (q < 4 || chalf == 0) : (q < 2 || chalf == 0);
+      const bool ok = !(PWC_STRIP_ABL & 1) && wr && keep;
       // nontemporal (aux 2): measured against sc1, nt sc1 and plain stores, 14.2 against
       // 17.0-19.9 us back to back (profiles/r04a_strip_store_policy.txt)
       // the last step's stores with PWC_STRIP_LAST_AUX (measurement builds)
-      __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + q * ostep : kOOB), 0,
+      __builtin_amdgcn_raw_buffer_store_b128(v, rso, (int)(ok ? o0 + pl[q] * plane_b : kOOB), 0,
                                              PF ? PWC_STRIP_STORE_AUX : PWC_STRIP_LAST_AUX);
     }
     CSTAMP(4 + 3 * st);  // stores issued
@@ -535,15 +592,15 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   }
   int ex;
   const float m = std::frexp(divisor, &ex);
-  if (m != 0.5f) return hipErrorNotSupported;  // the epilogue multiplies by 1 / divisor exactly
-  const float inv = std::ldexp(1.f, 1 - ex);
+  // a power-of-two divisor is an exact multiply; otherwise the kernel divides (inv = 0)
+  const float inv = m == 0.5f ? std::ldexp(1.f, 1 - ex) : 0.f;
   const OutEpi epi = current_epi();
   if (!(epi.slope <= 1.f)) return hipErrorNotSupported;  // max(v, slope v) form
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
   hipExtLaunchKernelGGL((corr_fwd_strip<G>), dim3((unsigned)nblk), dim3(G::THREADS),
                         G::LDS_ALLOC, stream, ev0, ev1, 0, (const float*)in1, (const float*)in2,
-                        (float*)out, H, W, ngrp, ntx, inv, epi);
+                        (float*)out, H, W, ngrp, ntx, inv, divisor, epi);
   return hipGetLastError();
 }
 
@@ -564,6 +621,9 @@ using GeoF = Geo<32, 6, 112, 2, 2, 1, true>;
 // C = 64, W = 56 (config 2 l3): the same whole-row form, 3 parity rows per workgroup (7 staged
 // f2 rows, 112 KB), one step of six compute waves
 using GeoF3 = Geo<64, 3, 56, 2, 3, 1, true>;
+// C = 96, W = 28 (config 2 l2): one parity row per workgroup (9 staged f2 rows, 136 KB), the
+// channels of a task in quarters (four compute waves, 24 channels per lane)
+using GeoF2 = Geo<96, 1, 28, 1, 1, 1, true, 4>;
 
 }  // namespace strip
 
@@ -572,10 +632,10 @@ using GeoF3 = Geo<64, 3, 56, 2, 3, 1, true>;
 // buffers, an output the kernel's 32-bit buffer addressing reaches, the max(v, slope v)
 // epilogue, and at least about one workgroup per CU (smaller grids leave CUs idle: the stream
 // and row-band kernels suit them better); C = 32 at W = 112 (whole rows) or a multiple of
-// 56 (strips), C = 64 at W = 56 (whole rows).  Knobs: strip=0 disables the kernel
+// 56 (strips), C = 64 at W = 56 and C = 96 at W = 28 (whole rows).  Knobs: strip=0 disables the kernel
 // (measurement of the stream / row-band kernels), strip_geo=4 selects the 56-px strips at
-// W = 112, strip_l3=0 leaves C = 64 to the row-band kernel.
-enum StripPlan : int { kStripNone = 0, kStripL4 = 1, kStripF = 2, kStripF3 = 3 };
+// W = 112, strip_l3=0 / strip_l2=0 leave C = 64 / 96 to the row-band kernel.
+enum StripPlan : int { kStripNone = 0, kStripL4 = 1, kStripF = 2, kStripF3 = 3, kStripF2 = 4 };
 static int strip_plan(const void* in1, const void* in2, const void* out, int B, int C, int H,
                       int W, int s2, int dtype, int layout) {
   if (dtype != 0 || s2 != 2 || layout != kRaster) return kStripNone;
@@ -596,6 +656,9 @@ static int strip_plan(const void* in1, const void* in2, const void* out, int B, 
   if (C == 64 && W == strip::GeoF3::TW && debug_knob("strip_l3", 1) != 0 &&
       strip::grid_blocks<strip::GeoF3>(B, H, W) >= 192)
     return kStripF3;
+  if (C == 96 && W == strip::GeoF2::TW && debug_knob("strip_l2", 1) != 0 &&
+      strip::grid_blocks<strip::GeoF2>(B, H, W) >= 192)
+    return kStripF2;
   return kStripNone;
 }
 
@@ -611,6 +674,8 @@ hipError_t corr_forward_strip(const void* in1, const void* in2, void* out, int B
       return strip::launch<strip::GeoF>(in1, in2, out, B, H, W, divisor, stream);
     case kStripF3:
       return strip::launch<strip::GeoF3>(in1, in2, out, B, H, W, divisor, stream);
+    case kStripF2:
+      return strip::launch<strip::GeoF2>(in1, in2, out, B, H, W, divisor, stream);
     case kStripL4:
       return strip::launch<strip::GeoL4>(in1, in2, out, B, H, W, divisor, stream);
     default:

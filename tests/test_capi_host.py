@@ -228,7 +228,8 @@ def test_corr_forward_plan_routes_and_declines():
     c9 = (9, 1, 9, 1, 2)
     assert plan(8, 32, 96, 112, *c9) == "strip"                # config 2 l4
     assert plan(8, 64, 48, 56, *c9) == "strip"                 # config 2 l3 (C = 64 rows)
-    assert plan(8, 96, 24, 28, *c9) == "rows"                  # config 2 l2
+    assert plan(8, 96, 24, 28, *c9) == "strip"                 # config 2 l2 (C = 96 quarters)
+    assert plan(6, 96, 24, 28, *c9) == "rows"                  # 144 workgroups: row bands
     assert plan(8, 192, 6, 7, *c9) == "band"                   # config 2 l0
     assert plan(16, 32, 112, 256, *c9, dtype=1) == "mstrip16"  # config 4 l4
     assert plan(16, 64, 56, 128, *c9, dtype=1) == "mstrip16"   # config 4 l3

@@ -81,6 +81,10 @@ FWD = [
     ("corr9", torch.float32, (6, 64, 48, 56), "strip C=64, B=6"),
     ("corr9", torch.float32, (8, 64, 46, 56), "strip C=64, partial row group"),
     ("corr9", torch.float32, (8, 64, 47, 56), "strip C=64, odd height"),
+    # C = 96 at W = 28 (GeoF2, config 2 l2: one parity row per workgroup, channel quarters):
+    # the shape and an odd height (parity rows 12 / 11)
+    ("corr9", torch.float32, (8, 96, 24, 28), "strip C=96 quarters (config 2 l2)"),
+    ("corr9", torch.float32, (8, 96, 23, 28), "strip C=96, odd height"),
     # the matrix-core fp16 strip kernel (corr_mstrip16.hip): its smallest batch at Sintel l4, a
     # partial last chunk (50 parity rows in chunks of 14) with a partial last strip (W = 200),
     # and an odd height (parity rows 50 / 49)
@@ -143,8 +147,9 @@ def test_cost_volume_448x1024_b4(shape):
     _check(out, O.cvl_forward(an, bn, 4), torch.float32)
 
 
-@pytest.mark.parametrize("shape,knob", [((8, 64, 48, 56), "strip_l3=0"),
-                                        ((8, 32, 96, 112), "strip_geo=4")], ids=["l3", "l4"])
+@pytest.mark.parametrize("shape,knob", [((8, 96, 24, 28), "strip_l2=0"),
+                                        ((8, 64, 48, 56), "strip_l3=0"),
+                                        ((8, 32, 96, 112), "strip_geo=4")], ids=["l2", "l3", "l4"])
 def test_strip_full_rows_after_other_kernels(shape, knob):
     """The whole-row strip geometries read each channel row's right halo from the next channel
     row's zero pad: a read issued before that pad's DMA group landed returns whatever LDS held
@@ -167,19 +172,21 @@ def test_strip_full_rows_after_other_kernels(shape, knob):
         _check(out, O.corr_forward(an, bn, 9, 1, 9, 1, 2), torch.float32)
 
 
-def test_strip_c64_into_cat_slice_leaky():
-    """model.py:83-84 + :89/91 at config 2's l3 (C = 64, 48 x 56, B = 8) through the strip
-    kernel's C = 64 whole-row geometry: the cat slice with leaky_relu(0.01) fused, and equal bit
-    for bit to the row-band kernel's volume (knob strip_l3=0) before the activation."""
+@pytest.mark.parametrize("shape,knob", [((8, 64, 48, 56), "strip_l3=0"),
+                                        ((8, 96, 24, 28), "strip_l2=0")], ids=["l3", "l2"])
+def test_strip_c64_into_cat_slice_leaky(shape, knob):
+    """model.py:83-84 + :89/91 at config 2's l3 / l2 (C = 64 / 96, B = 8) through the strip
+    kernel's whole-row geometries: the cat slice with leaky_relu(0.01) fused; the row-band
+    kernel's volume (knob) against the oracle too."""
     from pwcnet_amd import _lib
     from pwcnet_amd.ops import corr_forward, corr_forward_into
-    B, C, H, W = 8, 64, 48, 56
-    a, an = _rand((B, C, H, W), torch.float32, "l3a")
-    b, bn = _rand((B, C, H, W), torch.float32, "l3b")
+    B, C, H, W = shape
+    a, an = _rand((B, C, H, W), torch.float32, "l3a", C)
+    b, bn = _rand((B, C, H, W), torch.float32, "l3b", C)
     cat = torch.full((B, C + 81 + 2, H, W), 7.0, device=DEV)
     corr_forward_into(a, b, cat[:, C:C + 81], 9, 1, 9, 1, 2, negative_slope=0.01)
     plain = corr_forward(a, b, 9, 1, 9, 1, 2)
-    _lib.set_debug("strip_l3=0")
+    _lib.set_debug(knob)
     try:
         rows = corr_forward(a, b, 9, 1, 9, 1, 2)
         torch.cuda.synchronize()

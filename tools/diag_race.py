@@ -12,7 +12,7 @@ from pwcnet_amd.ops import corr_forward, warp_forward  # noqa: E402
 
 dev = torch.device("cuda:0")
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 100
-for lvl, knob in ((3, "strip_l3=0"), (4, "strip_geo=4")):
+for lvl, knob in ((2, "strip_l2=0"), (3, "strip_l3=0"), (4, "strip_geo=4")):
     C, h, w = bench.level_shapes(384, 448)[lvl]
     B = 8
     g = torch.Generator(device=dev).manual_seed(11)
