@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 profile -> $OUT (default gpurun_out/prof_r04): GPU suite under a kernel trace (+ kernel
+# Round profile -> $OUT (default gpurun_out/prof): GPU suite under a kernel trace (+ kernel
 # coverage), smoke, the default bench (live PMC, CPU baselines, Corr4 line, Net forward), its
 # rocprofv3 kernel stats, the training step (+ kernel stats), config 4 (+ kernel stats), and
 # the strip kernels' standalone timing / census.  Every GPU step under its own time limit.
 set -o pipefail
-OUT=${OUT:-gpurun_out/prof_r04}
+OUT=${OUT:-gpurun_out/prof}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/tests_trace -o run --output-format csv -- python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ --deselect tests/test_gpu_multirank.py::test_two_ranks_on_one_gpu_over_gloo > $OUT/gputests.txt 2>&1 || { tail -30 $OUT/gputests.txt; exit 1; }
