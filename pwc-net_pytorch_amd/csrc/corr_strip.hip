@@ -1,37 +1,38 @@
-// corr_strip.hip — correlation forward for the l4-sized fp32 grids of model.py:24's
-// Correlation(9, 1, 9, 1, 2) (BASELINE config 2 l4: 32 x 96 x 112, B = 8): output rows are
-// produced in STEPS so that their stores drain while the next rows compute.
+// corr_strip.hip — correlation forward for the strip-sized fp32 grids of model.py:24's
+// Correlation(9, 1, 9, 1, 2): BASELINE config 2's l4 (32 x 96 x 112), l3 (64 x 48 x 56) and l2
+// (96 x 24 x 28) at B = 8.  Output rows are produced in STEPS so that their stores drain while
+// the next rows compute.
 //
-// Semantics (correlation_cuda_kernel.cu:34-106 with k = 1, s1 = 1, pad = md = 9, s2 = 2, C = 32):
+// Semantics (correlation_cuda_kernel.cu:34-106 with k = 1, s1 = 1, pad = md = 9, s2 = 2):
 //   out[n, (tj+4)*9 + (ti+4), y, x] = sum_c f1[n,c,y,x] * f2[n,c,y+2tj,x+2ti] / C
 // with zeros outside the image (the reference's zero-padded scratch).
 //
-// Why this shape (DESIGN.md §4).  corr_stream.hip streams the channels of a 3-row band through
-// an LDS ring; every output needs the last channel, so the 28 MB of output only starts to
-// drain after the loop and ~9 us of each launch is a store phase with nothing under it.  Here a
-// workgroup owns a column STRIP (56 px) of R = 6 parity rows, and ALL channels of the R + 8 f2
-// parity rows it meets stay resident in LDS (14 rows x 32 ch x 72 px x 4 B = 129 KB).  The
-// rows are then produced two at a time in R / 2 = 3 steps: step s computes parity rows 2s and
-// 2s+1 of the strip (f2 rows 2s .. 2s+9), reduces, and issues its stores straight from the
-// registers, and step s+1 starts computing at once — its loads were staged during step s — so
-// two thirds of the output drains under compute.  Step 0's f2 rows arrive channel pair by
-// channel pair (the loader's first DMAs bring the first channels of all ten window rows), so
-// step 0 computes behind the loads the way the ring kernel does.
+// Why this shape (DESIGN.md §4.1).  corr_stream.hip streams the channels of a 3-row band through
+// an LDS ring; every output needs the last channel, so the l4 output only starts to drain after
+// the loop.  Here a workgroup owns R parity rows of one image parity over a column strip (or the
+// whole row), and ALL channels of the R + 8 f2 parity rows it meets stay resident in LDS.  The
+// rows are produced NQD at a time: step s computes its rows, reduces, and issues the stores
+// straight from the registers, and step s+1 starts at once (its rows were staged during step s).
+// Step 0's f2 rows arrive channel pair by channel pair (the loader's first DMAs bring the first
+// channels of every step-0 row), so step 0 computes behind the loads.
 //
-//   * loader wave: 14 rows x 9 LDS-DMAs (buffer_load_dwordx4 ... lds, 1 KiB each; the buffer
-//     range check gives the zero border), <= 63 in flight, one s_barrier per landed group.
-//   * compute waves: two quads of four (quad q takes parity rows 2s + q); lane = (tj, 4-px
-//     segment, channel half): per channel 5 ds_read_b128 of the f2 window and 18 v_pk_fma_f32
-//     on f1 values held in registers (loaded by the lane itself, the next step's f1 prefetched
-//     into the register of the channel just consumed).  The two channel halves of a task sit in
-//     lanes l and l+32 and are summed by v_permlane32_swap (one swap + one add per accumulator
-//     pair).  9 tj x 14 segments = 126 tasks -> 4 waves of 32 task slots per quad.
-//   * LDS rows are 590 quads apart (= 14 mod 16): every ds_read_b128 lane group of the lane map
-//     hits 16 distinct 16-B bank slots (conflict-free; checked by tools/strip_conflicts.py).
+// Geometries (struct Geo): GeoL4 = 56-px strips of 6 rows (round 4); GeoF = whole 112-px rows
+// (whole 448-B output rows: no 128-B line is shared by two workgroups), 6 rows in 3 steps, the
+// 81 (tj, segment) tasks of a row split into two workgroups by displacement row; GeoF3 (C = 64,
+// l3) = 3 rows in one step; GeoF2 (C = 96, l2) = 1 row, channels split in quarters.
+//
+//   * loader wave: each staged f2 row = whole 1-KiB LDS-DMAs (buffer_load_dwordx4 ... lds; the
+//     buffer range check gives the zero border), <= 63 in flight, one s_barrier per landed group.
+//   * compute waves: NQD groups of WPP waves (group q takes row NQD s + q); lane = (tj, 4-px
+//     segment, channel part): per channel 5 ds_read_b128 of the f2 window and 18 v_pk_fma_f32
+//     on f1 values the lane loaded itself (the next step's f1 prefetched into the register of
+//     the channel just consumed).  Channel halves sit in lanes l and l + 32 and are summed by
+//     v_permlane32_swap; quarters additionally by v_permlane16_swap.
+//   * LDS row stride = NSEG (mod 16) quads: every ds_read_b128 lane group hits 16 distinct 16-B
+//     bank slots (conflict-free; PMC SQ_LDS_BANK_CONFLICT = 0).
 //   * stores: 16 B per lane (4 px of one displacement plane), consecutive segments in
-//     consecutive lanes (224-B runs), nontemporal; 5 (low half) / 4 (high half) per step.
-//   * blocks are remapped XCD-aware so the strips of one image parity share an L2 (their f2
-//     rows overlap between row groups and at the strip halo).
+//     consecutive lanes, nontemporal.
+//   * blocks are remapped XCD-aware so the workgroups of one image parity share an L2.
 #include <hip/hip_ext.h>
 
 #include <cmath>

@@ -8,7 +8,7 @@ OUT=${OUT:-gpurun_out/prof}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/tests_trace -o run --output-format csv -- python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ --deselect tests/test_gpu_multirank.py::test_two_ranks_on_one_gpu_over_gloo > $OUT/gputests.txt 2>&1 || { tail -30 $OUT/gputests.txt; exit 1; }
-tail -2 $OUT/gputests.txt
+grep -E 'passed|failed' $OUT/gputests.txt
 # the two-rank rehearsal spawns its own ranks: outside the profiler
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_multirank.py > $OUT/gputests_multirank.txt 2>&1 || { tail -30 $OUT/gputests_multirank.txt; exit 1; }
 tail -1 $OUT/gputests_multirank.txt
