@@ -59,7 +59,7 @@ extern "C" {
 /* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
  * 4: fused warp -> correlation, 5: fused flow upsample -> warp, corr into a slice,
  * 6: pwc_set_debug, 7: grouped warp / warp -> correlation launches, 8: one-launch warp
- * backward with a workspace, 9: pwc_corr_forward_plan). */
+ * backward with a workspace, 9: pwc_corr_forward_plan, 10: pwc_corr_backward_plan). */
 PWC_API int pwc_abi_version(void);
 
 /* Which kernel family pwc_corr_forward would launch for these arguments (the same dispatch
@@ -75,6 +75,17 @@ PWC_API int pwc_abi_version(void);
 PWC_API int pwc_corr_forward_plan(const void* in1, const void* in2, const void* out, int B,
                                   int C, int H, int W, int pad_size, int kernel_size,
                                   int max_displacement, int stride1, int stride2, int dtype);
+
+/* Which kernel family pwc_corr_backward would launch (same predicates; no device call), -1 for
+ * arguments it rejects.  Replaces nothing in the reference (cu:417-473 launches two kernels). */
+#define PWC_BWD_PLAN_OTHER 0 /* stencil / tiled / generic kernels (corr_bwd.hip) */
+#define PWC_BWD_PLAN_ROWS 1  /* row bands with tj partials (corr_bwd_rows.hip; shapes it cannot
+                                band fall back to the stencil kernels) */
+#define PWC_BWD_PLAN_STRIP 2 /* displacement-row steps over resident rows (corr_bwd_strip.hip) */
+PWC_API int pwc_corr_backward_plan(const void* in1, const void* in2, const void* grad_out,
+                                   const void* grad_in1, const void* grad_in2, int B, int C,
+                                   int H, int W, int pad_size, int kernel_size,
+                                   int max_displacement, int stride1, int stride2, int dtype);
 
 /* Measurement hook: the next correlation dispatch of the calling thread that runs the l4-class
  * LDS-DMA kernel is launched with hipExtLaunchKernel, recording `start_event` / `stop_event`

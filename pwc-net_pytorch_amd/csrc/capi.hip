@@ -148,11 +148,13 @@ namespace pwc {
 bool corr_strip_accepts(const void*, const void*, const void*, int, int, int, int, int, int, int);
 bool corr_mstrip16_accepts(const void*, const void*, const void*, int, int, int, int, int, int,
                            int);
+bool corr_bwd_strip_accepts(const void*, const void*, const void*, const void*, const void*, int,
+                            int, int, int);
 }  // namespace pwc
 
 extern "C" {
 
-int pwc_abi_version(void) { return 9; }
+int pwc_abi_version(void) { return 10; }
 
 int pwc_corr_forward_plan(const void* in1, const void* in2, const void* out, int B, int C, int H,
                           int W, int pad_size, int kernel_size, int max_displacement, int stride1,
@@ -176,6 +178,25 @@ int pwc_corr_forward_plan(const void* in1, const void* in2, const void* out, int
   if (pwc::corr_strip_accepts(in1, in2, out, B, C, H, W, stride2, dtype, pwc::kRaster))
     return PWC_PLAN_STRIP;
   return PWC_PLAN_STREAM;
+}
+
+int pwc_corr_backward_plan(const void* in1, const void* in2, const void* grad_out,
+                           const void* grad_in1, const void* grad_in2, int B, int C, int H, int W,
+                           int pad_size, int kernel_size, int max_displacement, int stride1,
+                           int stride2, int dtype) {
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W) || stride1 != 1 ||
+      !corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo) ||
+      Ho <= 0 || Wo <= 0 || dtype < PWC_DTYPE_F32 || dtype > PWC_DTYPE_BF16)
+    return -1;
+  // the model configuration's fp32 kernels (corr_backward_t, corr_bwd.hip)
+  if (force_generic() != 0 || dtype != PWC_DTYPE_F32 || kernel_size != 1 || stride2 != 2 ||
+      pad_size != max_displacement || (max_displacement != 8 && max_displacement != 9))
+    return PWC_BWD_PLAN_OTHER;
+  if (pwc::corr_bwd_strip_accepts(in1, in2, grad_out, grad_in1, grad_in2, B, C, H, W))
+    return PWC_BWD_PLAN_STRIP;
+  return pwc::debug_knob("bwd_rows", 1) != 0 ? PWC_BWD_PLAN_ROWS : PWC_BWD_PLAN_OTHER;
 }
 
 int pwc_set_debug(const char* spec) {

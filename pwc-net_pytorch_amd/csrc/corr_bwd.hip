@@ -153,6 +153,11 @@ __global__ void corr_bwd_generic(const T* __restrict__ in1, const T* __restrict_
   }
 }
 
+// corr_bwd_strip.hip: model.py:24's configuration at the strip-sized levels (config 5 l3/l4),
+// fp32; it declines everything else.
+hipError_t corr_backward_strip_f32(const void* in1, const void* in2, const void* gout, void* g1,
+                                   void* g2, int B, int C, int H, int W, float divisor,
+                                   hipStream_t stream);
 // corr_bwd_rows.hip: model.py:24's configuration (stride-2 displacements, pad == md), fp32.
 hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* gout, void* g1,
                                   void* g2, int B, int C, int H, int W, float divisor,
@@ -169,8 +174,9 @@ hipError_t corr_backward_t(const void* in1, const void* in2, const void* gout, v
   if (npix == 0 || C == 0) return hipSuccess;
   if (force_generic == 0 && sizeof(T) == 4 && k == 1 && s1 == 1 && s2 == 2 && pad == md &&
       (md == 8 || md == 9) && layout == kRaster) {
-    const hipError_t e = corr_backward_rows_f32(in1, in2, gout, g1, g2, B, C, H, W, divisor,
-                                                stream);
+    hipError_t e = corr_backward_strip_f32(in1, in2, gout, g1, g2, B, C, H, W, divisor, stream);
+    if (e != hipErrorNotSupported) return e;
+    e = corr_backward_rows_f32(in1, in2, gout, g1, g2, B, C, H, W, divisor, stream);
     if (e != hipErrorNotSupported) return e;
   }
   if (force_generic != 1 && k == 1 && s1 == 1) {

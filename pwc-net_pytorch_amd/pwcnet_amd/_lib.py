@@ -51,6 +51,7 @@ class CorrProblem(ctypes.Structure):
 SYMBOLS = {
     "pwc_abi_version": (_I, []),
     "pwc_corr_forward_plan": (_I, [_P, _P, _P] + [_I] * 10),
+    "pwc_corr_backward_plan": (_I, [_P] * 5 + [_I] * 10),
     "pwc_last_error": (ctypes.c_char_p, []),
     "pwc_time_next_corr": (_I, [_P, _P]),
     "pwc_set_debug": (_I, [ctypes.c_char_p]),
@@ -78,7 +79,7 @@ SYMBOLS = {
     "pwc_corr_forward_into": (_I, [_P, _P, _P, ctypes.c_longlong, ctypes.c_float] + [_I] * 11
                               + [_P, _Z, _P]),
 }
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lock = threading.Lock()
 _lib = None
@@ -135,6 +136,16 @@ def corr_forward_plan(B, C, H, W, pad, k, md, s1, s2, dtype=0, ptrs=(0x1000, 0x2
     """Kernel family pwc_corr_forward would launch (pwc_corr_forward_plan; no device call)."""
     r = load().pwc_corr_forward_plan(*ptrs, B, C, H, W, pad, k, md, s1, s2, dtype)
     return PLAN_NAMES.get(r, r)
+
+
+BWD_PLAN_NAMES = {0: "other", 1: "rows", 2: "strip"}
+
+
+def corr_backward_plan(B, C, H, W, pad, k, md, s1, s2, dtype=0,
+                       ptrs=(0x1000, 0x2000, 0x3000, 0x4000, 0x5000)):
+    """Kernel family pwc_corr_backward would launch (pwc_corr_backward_plan; no device call)."""
+    r = load().pwc_corr_backward_plan(*ptrs, B, C, H, W, pad, k, md, s1, s2, dtype)
+    return BWD_PLAN_NAMES.get(r, r)
 
 
 def set_debug(spec: str = "") -> None:

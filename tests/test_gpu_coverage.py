@@ -411,3 +411,52 @@ def test_warp_fp16_alignment(case):
     _check(out, O.warp_forward(xn, fn), torch.float16)
     if case == "odd_offset":
         assert torch.equal(out, warp_forward(x, f))
+
+
+# corr_bwd_strip.hip (config 5's l4 / l3 backward): whole batches at the geometries' shapes, odd
+# heights (the odd-row parity has a band fewer / a short band), a height below one band, batch
+# 1; against the oracle, and repeatable bit for bit.
+BWD_STRIP = [(1, 32, 96, 112), (2, 32, 95, 112), (1, 32, 6, 112), (1, 32, 14, 112),
+             (2, 64, 48, 56), (1, 64, 47, 56), (3, 64, 10, 56)]
+
+
+@pytest.mark.parametrize("shape", BWD_STRIP, ids=lambda s: "x".join(map(str, s)))
+def test_corr_backward_strip_vs_oracle(shape):
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_backward
+    B, C, H, W = shape
+    assert _lib.corr_backward_plan(B, C, H, W, *CFG["corr9"]) == "strip"
+    a, an = _rand(shape, torch.float32, "sba", shape)
+    b, bn = _rand(shape, torch.float32, "sbb", shape)
+    g, gn = _rand((B, 81, H, W), torch.float32, "sbg", shape)
+    g1, g2 = corr_backward(a, b, g, *CFG["corr9"])
+    torch.cuda.synchronize()
+    r1, r2 = O.corr_backward(an, bn, gn, *CFG["corr9"])
+    _check(g1, r1, torch.float32, bwd=True)
+    _check(g2, r2, torch.float32, bwd=True)
+    h1, h2 = corr_backward(a, b, g, *CFG["corr9"])
+    torch.cuda.synchronize()
+    assert torch.equal(g1, h1) and torch.equal(g2, h2)
+
+
+@pytest.mark.parametrize("level", [3, 4])
+def test_corr_backward_strip_full_batch_vs_rows(level):
+    """BASELINE config 5 (B = 8, 384x448) at l3 / l4: the strip backward against the row-band
+    kernel (knob bwd_strip=0) on the same inputs, within fp32 summation-order differences."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_backward
+    C, H, W = {3: (64, 48, 56), 4: (32, 96, 112)}[level]
+    shape = (8, C, H, W)
+    a, _ = _rand(shape, torch.float32, "fba", level)
+    b, _ = _rand(shape, torch.float32, "fbb", level)
+    g, _ = _rand((8, 81, H, W), torch.float32, "fbg", level)
+    g1, g2 = corr_backward(a, b, g, *CFG["corr9"])
+    _lib.set_debug("bwd_strip=0")
+    try:
+        r1, r2 = corr_backward(a, b, g, *CFG["corr9"])
+    finally:
+        _lib.set_debug("")
+    torch.cuda.synchronize()
+    for x, y in ((g1, r1), (g2, r2)):
+        err = float((x - y).abs().max()) / float(y.abs().max())
+        assert err < 1e-5, err
