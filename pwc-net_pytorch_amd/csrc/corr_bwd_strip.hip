@@ -129,10 +129,18 @@ __device__ __forceinline__ f32x2 lds_rd2(uint32_t a) {
 // LDS reads could move across it)
 __device__ __forceinline__ void wg_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+#ifndef PWC_BSTRIP_GO_AUX  // cache policy of the gO DMAs (measurement builds may override)
+#define PWC_BSTRIP_GO_AUX 0
+#endif
+#ifndef PWC_BSTRIP_F_AUX  // cache policy of the feature-row DMAs
+#define PWC_BSTRIP_F_AUX 0
+#endif
+
+template <int AUX = 0>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t lds, uint32_t voff) {
 #if defined(__HIP_DEVICE_COMPILE__)
   __builtin_amdgcn_raw_ptr_buffer_load_lds(
-      rs, (__attribute__((address_space(3))) void*)(uintptr_t)lds, 16, voff, 0, 0, 0);
+      rs, (__attribute__((address_space(3))) void*)(uintptr_t)lds, 16, voff, 0, 0, AUX);
 #endif
 }
 
@@ -206,7 +214,7 @@ __device__ __forceinline__ void body(const Args& a, int n, int p, int band, int 
 #pragma unroll
       for (int i = 0; i < G::IPS; ++i) {
         if (D0 + i >= 63) asm volatile("s_waitcnt vmcnt(62)" ::: "memory");
-        dma16(rs, dst + (uint32_t)i * 1024u, relw[i]);
+        dma16<PWC_BSTRIP_F_AUX>(rs, dst + (uint32_t)i * 1024u, relw[i]);
       }
     };
     // prologue: steps 0 and 1 (rows 0 .. R), wait for step 0's
@@ -253,7 +261,7 @@ __device__ __forceinline__ void body(const Args& a, int n, int p, int band, int 
         const uint32_t off =
             ok ? relg[i] + (uint32_t)plane0 * plane_b + (uint32_t)(2 * Y + p) * (uint32_t)W * 4u
                : kOOB;
-        dma16(rsg, dst + (uint32_t)i * 1024u, off);
+        dma16<PWC_BSTRIP_GO_AUX>(rsg, dst + (uint32_t)i * 1024u, off);
       }
     };
     dma_g(0);
