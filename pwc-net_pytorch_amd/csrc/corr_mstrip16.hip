@@ -71,16 +71,23 @@ constexpr int row_halves(int nu) { return 2 * (16 * ((nu + 8 - 8 + 31) / 32) + 8
 // config-4 l2: <96, 32, 4, 24> (one 16-u block, rows split 2 + 1 x 7 over eight waves; K = 96
 // as three MFMAs; rows of 24 halves, NU + 8, so the ring fits the LDS -- at the cost of 2-way
 // bank conflicts on some transposed reads: RS_ overrides the conflict-free stride).
-template <int C_, int TW_, int RCH_, int RS_ = 0>
+// S1: stride-1 displacements (Correlation(4, 1, 4, 1, 1), CostVolumeLayer sr = 4): no column
+// parity -- a staged row is ONE plane of the strip's pixels x0 - 8 .. x0 + TW + 8, the two tiles
+// of a wave (the parities of stride 2) are two adjacent 16-px blocks, and the rows of the ring
+// are consecutive image rows instead of one parity's.
+template <int C_, int TW_, int RCH_, int RS_ = 0, bool S1_ = false>
 struct Geo {
   static constexpr int C = C_, TW = TW_, RCH = RCH_;
+  static constexpr bool S1 = S1_;
+  static constexpr int HALO = S1 ? TW_ / 2 + 16 : 8;  // staged halves beyond NU of an f2 row
   static constexpr int KC = C / 32;                // MFMA K chunks
   static constexpr int NU = TW / 2;                // pixels per parity
   static constexpr int NUB = NU / 16;              // 16-u blocks
   static constexpr int TS = 8 / NUB;               // displacement-row splits per block
   static constexpr int RS = RS_ ? RS_ : row_halves(NU);
-  static constexpr int EB = C * RS * 2;            // bytes per parity plane of a staged row
-  static constexpr int ROWB = 2 * EB;              // bytes per staged row
+  // bytes from a row's parity-0 data to its parity-1 data (stride 1: to the next 16-px block)
+  static constexpr int EB = S1 ? 32 : C * RS * 2;
+  static constexpr int ROWB = S1 ? C * RS * 2 : 2 * EB;  // bytes per staged row
   static constexpr int NSL = 11;                   // f2 ring: a step's 9 rows + 2 staged ahead
   static constexpr int LDS_BYTES = (NSL + 2) * ROWB;
   static constexpr int NWC = NUB * TS;             // compute waves
@@ -95,13 +102,18 @@ struct Geo {
   static constexpr int NK1 = (IF1 + LT - 1) / LT;
   static constexpr int LB = NK2 + NK1;
   static_assert(NWC == 8 && NUB * 16 == NU && C % 32 == 0, "eight compute waves, 16-u blocks");
-  static_assert((RS_ != 0 || (RS / 2) % 16 == 8) && RS >= NU + 8 && RS % 4 == 0,
+  static_assert((RS_ != 0 || (RS / 2) % 16 == 8) && RS >= NU + HALO && RS % (S1 ? 8 : 4) == 0,
                 "8 channel rows on distinct bank groups (unless overridden)");
   static_assert(LDS_BYTES <= 160 * 1024 && THREADS <= 1024, "workgroup resources");
 };
 using GeoL4 = Geo<32, 128, 14>;
 using GeoL3 = Geo<64, 64, 7>;
 using GeoL2 = Geo<96, 32, 4, 24>;
+// stride 1 (Corr4 / CostVolumeLayer) at config-4 l4 and l3: 14 / 7 image rows per workgroup;
+// rows of TW + 16 halves, (RS / 2) = 8 (mod 16) dwords as above
+using GeoS1L4 = Geo<32, 128, 14, 144, true>;
+using GeoS1L3 = Geo<64, 64, 7, 80, true>;
+using GeoS1L2 = Geo<96, 32, 4, 48, true>;
 
 constexpr uint32_t kOOB = 0x80000000u;
 
@@ -109,6 +121,7 @@ struct Ctx {
   __amdgpu_buffer_rsrc_t rs1, rs2;  // this image's f1 / f2
   uint32_t plane_b;                 // channel plane bytes
   int H, W, Y0, py, x0;
+  bool s1;                          // stride 1: rows are image rows, not one parity's
 };
 
 // A loader lane's items of one step: NK2 slots of the new f2 row (item i = lane + LT k, channel
@@ -122,6 +135,13 @@ struct LaneItems {
   int l[G::LB];       // LDS byte of its even run within a staged row, -1: no item
 };
 
+// Stride 1: LDS byte (within a staged row) of the 8 px at x = x0 + d of channel ch: f2 rows hold
+// pixels x0 - 8 .., f1 rows x0 ..
+template <class G>
+__device__ __forceinline__ int s1_byte(int ch, int d, bool f2) {
+  return (ch * G::RS + d + (f2 ? 8 : 0)) * 2;
+}
+
 template <class G>
 __device__ __forceinline__ void lane_items(const Ctx& c, int lt, LaneItems<G>& it) {
 #pragma unroll
@@ -133,13 +153,16 @@ __device__ __forceinline__ void lane_items(const Ctx& c, int lt, LaneItems<G>& i
     const int x = f2 ? c.x0 - 8 + 8 * kk : c.x0 + 8 * kk;
     const bool have = f2 ? i < G::IF2 : i < G::IF1;
     it.g[k] = have && x >= 0 && x < c.W ? (uint32_t)ch * c.plane_b + (uint32_t)x * 2u : kOOB;
-    it.l[k] = have ? (ch * G::RS + 4 * kk) * 2 : -1;
+    if constexpr (G::S1)
+      it.l[k] = have ? s1_byte<G>(ch, x - c.x0, f2) : -1;
+    else
+      it.l[k] = have ? (ch * G::RS + 4 * kk) * 2 : -1;
   }
 }
 
 // row term of parity row pr: byte offset of its first pixel, or kOOB outside the image
 __device__ __forceinline__ uint32_t row_off(const Ctx& c, int pr) {
-  const int y = 2 * pr + c.py;
+  const int y = c.s1 ? pr : 2 * pr + c.py;
   return pr >= 0 && y < c.H ? (uint32_t)y * (uint32_t)c.W * 2u : kOOB;
 }
 
@@ -149,9 +172,14 @@ __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t rs, uint32_t g, u
 }
 
 // 8 pixels of one channel -> the 4 even and the 4 odd halves, one 8-B run in each parity plane
+// (stride 1: the 8 pixels as they are)
 template <class G>
 __device__ __forceinline__ void item_store(char* lds, int lds_b, const u32x4& d) {
   if (lds_b < 0) return;
+  if constexpr (G::S1) {
+    *reinterpret_cast<u32x4*>(lds + lds_b) = d;
+    return;
+  }
   const u32x2 ev = {__builtin_amdgcn_perm(d.y, d.x, 0x05040100u),
                     __builtin_amdgcn_perm(d.w, d.z, 0x05040100u)};
   const u32x2 od = {__builtin_amdgcn_perm(d.y, d.x, 0x07060302u),
@@ -240,7 +268,8 @@ __device__ __forceinline__ void read_b(const char* lds, int f2b, BOps<G>& b) {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int k = 0; k < G::KC; ++k)
-        b.v[e][h][k] = tr_block<G>(lds, f2b + e * G::EB + 16 * h + k * 32 * G::RS * 2);
+        b.v[e][h][k] =
+            tr_block<G>(lds, f2b + e * G::EB + 16 * h + (G::S1 ? 8 : 0) + k * 32 * G::RS * 2);
 }
 
 // Displacement rows TJ0 .. TJ0 + NTJ - 1 of one output row: the next row's operand blocks are
@@ -250,7 +279,7 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
                                         const f16x8 (&a)[2][2][G::KC], bool plain,
                                         float inv_divisor, float divisor, float slope,
                                         __amdgpu_buffer_rsrc_t rso, uint32_t o0, uint32_t pstep,
-                                        bool lane_ok, int jj, int abl) {
+                                        bool lane_ok, int jj, int abl, int layout) {
   if (MS_ABL(1)) {
     const u32x4 h = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -281,11 +310,45 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
     f32x4 e[2];
 #pragma unroll
     for (int pe = 0; pe < 2; ++pe) {
-      // exact 2^-k multiply, or the reference's fp32 division when C is not a power of two
+      // exact 2^-k multiply; otherwise (C = 96, CostVolumeLayer's / 81) the quotient from the
+      // reciprocal with one Newton correction (q + (r - q d) / d): within an fp32 ulp of the
+      // division, which the fp16 rounding of the stored value absorbs -- a tenth of a division's
+      // instructions
       const f32x4 r = diag(d[pe]);
-      e[pe] = inv_divisor != 0.f ? r * inv_divisor
-                                 : f32x4{r[0] / divisor, r[1] / divisor, r[2] / divisor,
-                                         r[3] / divisor};
+      if (inv_divisor != 0.f) {
+        e[pe] = r * inv_divisor;
+      } else {
+        const float rcp = 1.f / divisor;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float q = r[v] * rcp;
+          e[pe][v] = __builtin_fmaf(__builtin_fmaf(-q, divisor, r[v]), rcp, q);
+        }
+      }
+    }
+    // output plane of (tj, ti = jj): raster (tj * 9 + ti) or CostVolumeLayer order (stride 1)
+    const uint32_t pl = G::S1 && layout == kCvl ? (uint32_t)cvl_channel(tj - 4, min(jj, 8) - 4, 4)
+                                                : (uint32_t)(tj * 9 + jj);
+    if constexpr (G::S1) {
+      // tile pe: pixels 32 ub + 16 pe + 4 g + v.  One permlane16 swap per dword gives lane row g
+      // eight consecutive pixels: even rows block 0's x 8 (g / 2) .., odd rows block 1's -- one
+      // 16-B store, 64 B per wave and plane (plain epilogue: the predicate declines a fused
+      // leaky_relu for stride 1)
+      uint32_t p0 = __builtin_bit_cast(uint32_t, h2_t{(_Float16)e[0][0], (_Float16)e[0][1]});
+      uint32_t p1 = __builtin_bit_cast(uint32_t, h2_t{(_Float16)e[0][2], (_Float16)e[0][3]});
+      uint32_t q0 = __builtin_bit_cast(uint32_t, h2_t{(_Float16)e[1][0], (_Float16)e[1][1]});
+      uint32_t q1 = __builtin_bit_cast(uint32_t, h2_t{(_Float16)e[1][2], (_Float16)e[1][3]});
+      asm volatile(
+          "s_nop 1\n\t"
+          "v_permlane16_swap_b32 %0, %2\n\t"
+          "v_permlane16_swap_b32 %1, %3\n\t"
+          "s_nop 1"
+          : "+v"(p0), "+v"(p1), "+v"(q0), "+v"(q1));
+      const u32x4 hs = {p0, p1, q0, q1};
+      __builtin_amdgcn_raw_buffer_store_b128(hs, rso, (int)(lane_ok ? o0 + pl * pstep : kOOB), 0,
+                                             2);
+      if (t + 1 < NTJ) bc = bn;
+      continue;
     }
     u32x4 h;
     if (plain) {
@@ -298,7 +361,7 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
         h[v] = __builtin_bit_cast(uint32_t, h2_t{(_Float16)fmaxf(e[0][v], e[0][v] * slope),
                                                  (_Float16)fmaxf(e[1][v], e[1][v] * slope)});
     }
-    const uint32_t off = o0 + (uint32_t)(tj * 9 + jj) * pstep;
+    const uint32_t off = o0 + pl * pstep;
     // nontemporal: the volume is read by the next layer, not by this kernel
     __builtin_amdgcn_raw_buffer_store_b128(h, rso, (int)(lane_ok ? off : kOOB), 0, 2);
     if (t + 1 < NTJ) bc = bn;
@@ -308,14 +371,16 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
 template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
     const __half* __restrict__ in1, const __half* __restrict__ in2, __half* __restrict__ out,
-    int H, int W, int nchunk, int ntx, float inv_divisor, float divisor, OutEpi epi, int abl) {
+    int H, int W, int nchunk, int ntx, float inv_divisor, float divisor, OutEpi epi, int abl,
+    int layout) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  // logical block = (n, row parity, chunk, strip), strip fastest (XCD neighbours share rows)
+  // logical block = (n, row parity, chunk, strip), strip fastest (XCD neighbours share rows);
+  // stride 1: (n, chunk, strip)
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int tx = t % ntx;
   const int ch = (t / ntx) % nchunk;
-  const int py = (t / (ntx * nchunk)) & 1;
-  const int n = t / (ntx * nchunk * 2);
+  const int py = G::S1 ? 0 : (t / (ntx * nchunk)) & 1;
+  const int n = t / (ntx * nchunk * (G::S1 ? 1 : 2));
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   Ctx c;
@@ -326,6 +391,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
   c.rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)img1, (short)0, (int)img_bytes, 0x00020000);
   c.rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)img2, (short)0, (int)img_bytes, 0x00020000);
   c.H = H, c.W = W, c.Y0 = ch * G::RCH, c.py = py, c.x0 = tx * G::TW;
+  c.s1 = G::S1;
 
   // step 0's window (f2 rows 0..8) and f1 row: every wave, one batch (item i of the 9 x IF2
   // window items: row i / IF2; then the f1 row)
@@ -344,7 +410,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
       r[k] = load16(c.rs2,
                     have && x >= 0 && x < W ? (uint32_t)chn * c.plane_b + (uint32_t)x * 2u : kOOB,
                     row_off(c, c.Y0 - 4 + m));
-      b[k] = have ? m * G::ROWB + (chn * G::RS + 4 * kk) * 2 : -1;
+      b[k] = !have ? -1
+                   : m * G::ROWB + (G::S1 ? s1_byte<G>(chn, x - c.x0, true)
+                                          : (chn * G::RS + 4 * kk) * 2);
     }
 #pragma unroll
     for (int k = 0; k < S1; ++k) {
@@ -355,7 +423,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
       r[SK + k] = load16(c.rs1,
                          have && x < W ? (uint32_t)chn * c.plane_b + (uint32_t)x * 2u : kOOB,
                          row_off(c, c.Y0));
-      b[SK + k] = have ? G::NSL * G::ROWB + (chn * G::RS + 4 * kk) * 2 : -1;
+      b[SK + k] = !have ? -1
+                        : G::NSL * G::ROWB + (G::S1 ? s1_byte<G>(chn, x - c.x0, false)
+                                                    : (chn * G::RS + 4 * kk) * 2);
     }
 #pragma unroll
     for (int k = 0; k < SK + S1; ++k) item_store<G>(lds, b[k], r[k]);
@@ -386,9 +456,11 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
   const int ub = wave % G::NUB;  // 16-u block: pixels x0 + 32 ub .. + 31
   const int th = wave / G::NUB;  // displacement-row split
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, jj = lane & 15;
-  const int lane_b = ((4 * g + q) * G::RS + 4 * p) * 2 + 32 * ub;
+  const int lane_b = ((4 * g + q) * G::RS + 4 * p) * 2 + (G::S1 ? 64 : 32) * ub;
   const bool lo_rows = (lane & 15) < 8;  // A rows 0-7 (lanes l & 15 < 8)
-  const int xs = c.x0 + 32 * ub + 8 * g;  // this lane's 8 output pixels
+  // this lane's 8 output pixels (stride 1 after the swap: block g & 1 of the wave's two, 8 (g / 2)
+  // into it)
+  const int xs = G::S1 ? c.x0 + 32 * ub + 16 * (g & 1) + 8 * (g >> 1) : c.x0 + 32 * ub + 8 * g;
   const bool lane_ok = jj < 9 && xs < W && !MS_ABL(2);
   const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * H * W)), (short)0,
@@ -399,7 +471,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
   int slot0 = 0;                                       // slot of window row s
   for (int s = 0; s < G::RCH; ++s) {
     __builtin_amdgcn_s_barrier();  // B_s: the step's rows are in LDS
-    const int y = 2 * (c.Y0 + s) + py;
+    const int y = G::S1 ? c.Y0 + s : 2 * (c.Y0 + s) + py;
     if (y < H) {
       const int f1b = (G::NSL + (s & 1)) * G::ROWB + lane_b;
       f16x8 a[2][2][G::KC];  // [parity][rows 0-7 | rows 8-15][K chunk]
@@ -416,7 +488,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
       // the 9 displacement rows split over TS waves per block: 5 + 4, or 3 + 2 + 2 + 2
 #define PWC_TJ(A, N)                                                                          \
   tj_rows<G, A, N>(lds, slot0, lane_b, a, plain, inv_divisor, divisor, slope, rso, o0, pstep,\
-                   lane_ok, jj, abl)
+                   lane_ok, jj, abl, layout)
       if constexpr (G::TS == 2) {
         if (th == 0)
           PWC_TJ(0, 5);
@@ -450,23 +522,28 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
   }
 }
 
+// workgroups of the grid: (n, row parity, chunk, strip), stride 1 without the parity
+template <class G>
+long long grid_blocks(int B, int H, int W) {
+  const int rows = G::S1 ? H : (H + 1) / 2;
+  return (long long)B * (G::S1 ? 1 : 2) * ((rows + G::RCH - 1) / G::RCH) *
+         ((W + G::TW - 1) / G::TW);
+}
+
 template <class G>
 bool accepts(const void* in1, const void* in2, const void* out, int B, int H, int W) {
   if ((uintptr_t)in1 % 16 || (uintptr_t)in2 % 16 || (uintptr_t)out % 16) return false;
   if (W % 8 || W < 64 || H < 2 || (size_t)G::C * H * W * 2 >= 0x7ffffff0ull) return false;
   if ((size_t)81 * H * W * 2 >= 0x7ffffff0ull) return false;
-  const long long nblk = (long long)B * 2 * (((H + 1) / 2 + G::RCH - 1) / G::RCH) *
-                         ((W + G::TW - 1) / G::TW);
-  return nblk >= 192;
+  return grid_blocks<G>(B, H, W) >= 192;
 }
 
 template <class G>
 hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int W, float inv,
-                  float divisor,
-                  const OutEpi& epi, hipStream_t stream) {
-  const int nchunk = ((H + 1) / 2 + G::RCH - 1) / G::RCH;
+                  float divisor, const OutEpi& epi, hipStream_t stream, int layout = kRaster) {
+  const int nchunk = ((G::S1 ? H : (H + 1) / 2) + G::RCH - 1) / G::RCH;
   const int ntx = (W + G::TW - 1) / G::TW;
-  const long long nblk = (long long)B * 2 * nchunk * ntx;
+  const long long nblk = grid_blocks<G>(B, H, W);
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   static bool attr_set = false;
@@ -486,7 +563,8 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int
   take_launch_events(&ev0, &ev1);  // bench.py's live timing hook (one-shot)
   hipExtLaunchKernelGGL((corr_fwd_mstrip16<G>), dim3((unsigned)nblk), dim3(G::THREADS),
                         G::LDS_BYTES, stream, ev0, ev1, 0, (const __half*)in1,
-                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, divisor, epi, abl);
+                        (const __half*)in2, (__half*)out, H, W, nchunk, ntx, inv, divisor, epi, abl,
+                        layout);
   return hipGetLastError();
 }
 
@@ -498,11 +576,23 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int
 // workgroup per CU, and an output epilogue the kernel writes itself (leaky_relu slope <= 1:
 // the max(v, slope v) form; a channel-slice stride that keeps 16-B stores aligned) -- so this
 // predicate, corr_forward_path and the launcher agree (knob mstrip16=0: off).
+// Stride 1 (Correlation(4, 1, 4, 1, 1) and CostVolumeLayer sr = 4; pad == md: the caller): C =
+// 32 / 64 / 96, raster or CostVolumeLayer channel order, a plain output (no fused epilogue, no
+// channel slice: those are the Corr9 model path's).
 bool corr_mstrip16_accepts(const void* in1, const void* in2, const void* out, int B, int C,
                            int H, int W, int s2, int dtype, int layout) {
-  if (dtype != 1 || s2 != 2 || layout != kRaster) return false;
-  if (debug_knob("mstrip16", 1) == 0) return false;
+  if (dtype != 1 || debug_knob("mstrip16", 1) == 0) return false;
   const OutEpi epi = current_epi();
+  if (s2 == 1) {
+    if ((layout != kRaster && layout != kCvl) || epi.slope != 1.f || epi.ostride != 0 ||
+        debug_knob("mstrip16_s1", 1) == 0)
+      return false;
+    if (C == 32) return mstrip16::accepts<mstrip16::GeoS1L4>(in1, in2, out, B, H, W);
+    if (C == 64) return mstrip16::accepts<mstrip16::GeoS1L3>(in1, in2, out, B, H, W);
+    if (C == 96) return mstrip16::accepts<mstrip16::GeoS1L2>(in1, in2, out, B, H, W);
+    return false;
+  }
+  if (s2 != 2 || layout != kRaster) return false;
   if (!(epi.slope <= 1.f) || epi.ostride % 8) return false;
   if (C == 32) return mstrip16::accepts<mstrip16::GeoL4>(in1, in2, out, B, H, W);
   if (C == 64) return mstrip16::accepts<mstrip16::GeoL3>(in1, in2, out, B, H, W);
@@ -511,14 +601,26 @@ bool corr_mstrip16_accepts(const void* in1, const void* in2, const void* out, in
 }
 
 hipError_t corr_forward_mstrip16(const void* in1, const void* in2, void* out, int B, int C,
-                                 int H, int W, float divisor, hipStream_t stream) {
-  if (!corr_mstrip16_accepts(in1, in2, out, B, C, H, W, 2, 1, kRaster))
+                                 int H, int W, int s2, int layout, float divisor,
+                                 hipStream_t stream) {
+  if (!corr_mstrip16_accepts(in1, in2, out, B, C, H, W, s2, 1, layout))
     return hipErrorNotSupported;
   int ex;
   const float mnt = std::frexp(divisor, &ex);
-  // a power-of-two divisor is an exact multiply; otherwise the kernel divides (inv = 0)
+  // a power-of-two divisor is an exact multiply; otherwise the kernel divides (inv = 0: the
+  // CostVolumeLayer's /81)
   const float inv = mnt == 0.5f ? std::ldexp(1.f, 1 - ex) : 0.f;
   const OutEpi epi = current_epi();  // slope and stride checked by the predicate
+  if (s2 == 1) {
+    if (C == 32)
+      return mstrip16::launch<mstrip16::GeoS1L4>(in1, in2, out, B, H, W, inv, divisor, epi,
+                                                 stream, layout);
+    if (C == 64)
+      return mstrip16::launch<mstrip16::GeoS1L3>(in1, in2, out, B, H, W, inv, divisor, epi,
+                                                 stream, layout);
+    return mstrip16::launch<mstrip16::GeoS1L2>(in1, in2, out, B, H, W, inv, divisor, epi, stream,
+                                               layout);
+  }
   if (C == 32) return mstrip16::launch<mstrip16::GeoL4>(in1, in2, out, B, H, W, inv, divisor, epi,
                                                               stream);
   if (C == 64) return mstrip16::launch<mstrip16::GeoL3>(in1, in2, out, B, H, W, inv, divisor, epi,

@@ -766,16 +766,18 @@ hipError_t corr_forward_strip(const void*, const void*, void*, int, int, int, in
                               hipStream_t);
 bool corr_mstrip16_accepts(const void*, const void*, const void*, int, int, int, int, int, int,
                            int);
-hipError_t corr_forward_mstrip16(const void*, const void*, void*, int, int, int, int, float,
-                                 hipStream_t);
+hipError_t corr_forward_mstrip16(const void*, const void*, void*, int, int, int, int, int, int,
+                                 float, hipStream_t);
 
 hipError_t corr_forward_stream(const void* in1, const void* in2, void* out, int B, int C, int H,
                                int W, int s2, int dtype, int layout, float divisor,
                                hipStream_t stream) {
-  // fp16 storage, C = 32 / 64 / 96 (config-4 l4 / l3 / l2): the matrix-core strip kernel
-  // (corr_mstrip16.hip), which also takes grids the stream kernel declines
+  // fp16 storage, C = 32 / 64 / 96 (config-4 l4 / l3 / l2; stride 1: C = 32 / 64): the
+  // matrix-core strip kernel (corr_mstrip16.hip), which also takes grids the stream kernel
+  // declines
   if (corr_mstrip16_accepts(in1, in2, out, B, C, H, W, s2, dtype, layout)) {
-    const hipError_t e = corr_forward_mstrip16(in1, in2, out, B, C, H, W, divisor, stream);
+    const hipError_t e =
+        corr_forward_mstrip16(in1, in2, out, B, C, H, W, s2, layout, divisor, stream);
     if (e != hipErrorNotSupported) return e;
   }
   // fp32 model-config grids of C = 32 (config 2 l4) and C = 64 at W = 56 (config 2 l3): the

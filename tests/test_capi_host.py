@@ -234,6 +234,10 @@ def test_corr_forward_plan_routes_and_declines():
     assert plan(16, 32, 112, 256, *c9, dtype=1) == "mstrip16"  # config 4 l4
     assert plan(16, 64, 56, 128, *c9, dtype=1) == "mstrip16"   # config 4 l3
     assert plan(8, 32, 96, 112, 4, 1, 4, 1, 1) == "stream"     # Corr4 at l4
+    assert plan(16, 32, 112, 256, 4, 1, 4, 1, 1, dtype=1) == "mstrip16"  # Corr4 fp16 config-4 l4
+    assert plan(16, 64, 56, 128, 4, 1, 4, 1, 1, dtype=1) == "mstrip16"   # ... l3
+    assert plan(16, 96, 28, 64, 4, 1, 4, 1, 1, dtype=1) == "mstrip16"    # ... l2
+    assert plan(8, 32, 112, 256, 4, 1, 4, 1, 1, dtype=1) == "stream"     # 128 workgroups
     # H*W = 8.4 M px: input 1.07 GB (< 2^31, the strip would accept it), output 2.7 GB
     assert plan(1, 32, 3000, 2800, *c9) == "stream"
     assert plan(1, 32, 3000, 2800, *c9, dtype=1) == "mstrip16"  # fp16 output 1.36 GB < 2^31

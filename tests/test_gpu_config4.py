@@ -152,3 +152,39 @@ def test_fused_band_fp16_group_pair_equals_single_calls():
     for (a, b, f), (c, w) in zip(probs, grouped):
         c1, w1 = warp_corr_forward(a, b, f, 9, 1, 9, 1, 2)
         assert torch.equal(c, c1) and torch.equal(w, w1)
+
+
+# Stride 1 (Correlation(4, 1, 4, 1, 1) and CostVolumeLayer sr = 4) on the matrix cores
+# (corr_mstrip16.hip, S1 geometries): config-4 l4 / l3 at B = 16, an odd height (a chunk cut
+# short), a width that is not a multiple of the 128-px strip (partial second strip), both channel
+# orders; against the oracle on the fp16 inputs within the fp16 output rounding, and against the
+# VALU stream kernel (knob mstrip16_s1=0).
+S1_CASES = [("corr4", (16, 32, 112, 256)), ("cvl", (16, 32, 112, 256)), ("corr4", (16, 64, 56, 128)),
+            ("cvl", (16, 64, 56, 128)), ("corr4", (16, 96, 28, 64)), ("cvl", (16, 96, 28, 64)),
+            ("corr4", (16, 32, 111, 256)), ("corr4", (24, 32, 56, 200))]
+
+
+@pytest.mark.parametrize("cfg,shape", S1_CASES, ids=lambda v: v if isinstance(v, str) else "x".join(map(str, v)))
+def test_stride1_matrix_cores_vs_oracle(cfg, shape):
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_forward, cost_volume_forward
+    B, C, H, W = shape
+    assert _lib.corr_forward_plan(B, C, H, W, 4, 1, 4, 1, 1, dtype=1) == "mstrip16"
+    rng = np.random.default_rng(90 + H + W + C)
+    a, b = _h(rng, *shape), _h(rng, *shape)
+
+    def run():
+        return corr_forward(a, b, 4, 1, 4, 1, 1) if cfg == "corr4" else cost_volume_forward(a, b, 4)
+    out = run()
+    torch.cuda.synchronize()
+    an, bn = _np(a), _np(b)
+    ref = O.corr_forward(an, bn, 4, 1, 4, 1, 1) if cfg == "corr4" else O.cvl_forward(an, bn, 4)
+    _close_rel(_np(out), ref, 2e-3)
+    _lib.set_debug("mstrip16_s1=0")
+    try:
+        alt = run()
+    finally:
+        _lib.set_debug("")
+    torch.cuda.synchronize()
+    err = float((out.float() - alt.float()).abs().max()) / float(alt.float().abs().max())
+    assert err <= 2e-3, err
