@@ -624,7 +624,10 @@ using GeoF = Geo<32, 6, 112, 2, 2, 1, true>;
 using GeoF3 = Geo<64, 3, 56, 2, 3, 1, true>;
 // C = 96, W = 28 (config 2 l2): one parity row per workgroup (9 staged f2 rows, 136 KB), the
 // channels of a task in quarters (four compute waves, 24 channels per lane)
-using GeoF2 = Geo<96, 1, 28, 1, 1, 1, true, 4>;
+#ifndef PWC_STRIP_GEOF2  // (measurement builds may override)
+#define PWC_STRIP_GEOF2 96, 1, 28, 1, 1, 1, true, 4
+#endif
+using GeoF2 = Geo<PWC_STRIP_GEOF2>;
 
 }  // namespace strip
 
