@@ -274,9 +274,12 @@ __device__ __forceinline__ void read_b(const char* lds, int f2b, BOps<G>& b) {
 
 // Displacement rows TJ0 .. TJ0 + NTJ - 1 of one output row: the next row's operand blocks are
 // read while this row's products, diagonals and store run.
-template <class G, int TJ0, int NTJ>
+// PLAIN: no fused leaky_relu; POW2: the divisor is a power of two (an exact multiply by
+// inv_divisor) -- both compile-time, so no uniform branch sits between the stores (a branch
+// around the epilogue cost the compiler its vmcnt accounting across the stores)
+template <class G, int TJ0, int NTJ, bool PLAIN, bool POW2>
 __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
-                                        const f16x8 (&a)[2][2][G::KC], bool plain,
+                                        const f16x8 (&a)[2][2][G::KC],
                                         float inv_divisor, float divisor, float slope,
                                         __amdgpu_buffer_rsrc_t rso, uint32_t o0, uint32_t pstep,
                                         bool lane_ok, int jj, int abl, int layout) {
@@ -315,7 +318,7 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
       // division, which the fp16 rounding of the stored value absorbs -- a tenth of a division's
       // instructions
       const f32x4 r = diag(d[pe]);
-      if (inv_divisor != 0.f) {
+      if constexpr (POW2) {
         e[pe] = r * inv_divisor;
       } else {
         const float rcp = 1.f / divisor;
@@ -351,7 +354,7 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
       continue;
     }
     u32x4 h;
-    if (plain) {
+    if constexpr (PLAIN) {
 #pragma unroll
       for (int v = 0; v < 4; ++v)
         h[v] = __builtin_bit_cast(uint32_t, h2_t{(_Float16)e[0][v], (_Float16)e[1][v]});
@@ -466,7 +469,9 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
       (void*)(out + (epi.ostride ? (size_t)n * epi.ostride : (size_t)n * 81 * H * W)), (short)0,
       (int)(81u * c.plane_b), 0x00020000);
   const float slope = epi.slope;
-  const bool plain = slope == 1.f;  // no fused leaky_relu
+  const bool plain = slope == 1.f;  // no fused leaky_relu (stride 1: always, the predicate)
+  // stride 2 divides by its compile-time C; stride 1 by C or, for CostVolumeLayer, 81
+  const bool pow2 = G::S1 ? inv_divisor != 0.f : (G::C & (G::C - 1)) == 0;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's share of step 0's staging
   int slot0 = 0;                                       // slot of window row s
   for (int s = 0; s < G::RCH; ++s) {
@@ -486,9 +491,24 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
       const uint32_t o0 = ((uint32_t)y * W + xs) * 2u;
       const uint32_t pstep = c.plane_b;
       // the 9 displacement rows split over TS waves per block: 5 + 4, or 3 + 2 + 2 + 2
+#define PWC_TJ1(A, N, PL, P2)                                                                 \
+  tj_rows<G, A, N, PL, P2>(lds, slot0, lane_b, a, inv_divisor, divisor, slope, rso, o0, pstep, \
+                           lane_ok, jj, abl, layout)
 #define PWC_TJ(A, N)                                                                          \
-  tj_rows<G, A, N>(lds, slot0, lane_b, a, plain, inv_divisor, divisor, slope, rso, o0, pstep,\
-                   lane_ok, jj, abl, layout)
+  do {                                                                                        \
+    if constexpr (G::S1) {                                                                    \
+      if (pow2)                                                                               \
+        PWC_TJ1(A, N, true, true);                                                            \
+      else                                                                                    \
+        PWC_TJ1(A, N, true, false);                                                           \
+    } else {                                                                                  \
+      constexpr bool P2 = (G::C & (G::C - 1)) == 0;                                           \
+      if (plain)                                                                              \
+        PWC_TJ1(A, N, true, P2);                                                              \
+      else                                                                                    \
+        PWC_TJ1(A, N, false, P2);                                                             \
+    }                                                                                         \
+  } while (0)
       if constexpr (G::TS == 2) {
         if (th == 0)
           PWC_TJ(0, 5);
@@ -517,6 +537,7 @@ __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_mstrip16(
           PWC_TJ(7, 2);
       }
 #undef PWC_TJ
+#undef PWC_TJ1
     }
     slot0 = slot0 + 1 == G::NSL ? 0 : slot0 + 1;
   }
@@ -611,6 +632,8 @@ hipError_t corr_forward_mstrip16(const void* in1, const void* in2, void* out, in
   // CostVolumeLayer's /81)
   const float inv = mnt == 0.5f ? std::ldexp(1.f, 1 - ex) : 0.f;
   const OutEpi epi = current_epi();  // slope and stride checked by the predicate
+  // stride 2 takes its power-of-two decision from C at compile time: Correlation's k^2 C, k = 1
+  if (s2 == 2 && divisor != (float)C) return hipErrorNotSupported;
   if (s2 == 1) {
     if (C == 32)
       return mstrip16::launch<mstrip16::GeoS1L4>(in1, in2, out, B, H, W, inv, divisor, epi,
