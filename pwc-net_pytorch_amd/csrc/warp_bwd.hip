@@ -56,16 +56,20 @@ __device__ unsigned long long g_wbwd_census[4096 * 16];
 // vmcnt waits -- see warp_bwd_tile)
 // Product builds compile the marks and the ablation bits out (`make CENSUS=1` keeps them).
 #ifdef PWC_CENSUS
-#define WB_MARK(k)                                                                          \
+#define WB_MARKC(k, cond)                                                                   \
   do {                                                                                      \
-    const bool on_ = a.census && threadIdx.x == 0 && blockIdx.x < 4096;                     \
+    const bool on_ = a.census && (cond) && threadIdx.x == 0 && blockIdx.x < 4096;           \
     const unsigned long long ts_ = __builtin_amdgcn_s_memrealtime();                        \
     __builtin_amdgcn_raw_buffer_store_b64(                                                  \
         __builtin_bit_cast(u32x2_t, ts_), census_rsrc(),                                    \
         on_ ? (int)((blockIdx.x * 16 + (k)) * 8) : (int)0x80000000, 0, 0);                  \
   } while (0)
+#define WB_MARK(k) WB_MARKC(k, true)
 #define WB_ABL(bit) (a.census & (bit))
 #else
+#define WB_MARKC(k, cond) \
+  do {                    \
+  } while (0)
 #define WB_MARK(k) \
   do {             \
   } while (0)
@@ -290,35 +294,56 @@ __global__ __launch_bounds__(NT, 2) void warp_bwd_tile(Args a) {
   __builtin_amdgcn_raw_buffer_store_b32((unsigned)nfar, rsfcnt,
                                         (t & 63) == 0 ? wave * 4 : (int)0x80000000, 0, 0);
   lds_barrier();  // the list is complete
-  // the first 8 list entries in registers for every chunk
-  constexpr int KE = 8;
+  // the first 12 list entries in registers for every chunk (random N(0, 2^2)-px flows give
+  // ~4 per tile pixel; 12 keeps the waves with a longer list rare at 4 waves per SIMD)
+  constexpr int KE = 12;
   int2 ent[KE];
 #pragma unroll
   for (int j = 0; j < KE; ++j) ent[j] = j < len ? lent[start + j] : int2{0, 0};
   WB_MARK(2);
 
   // one chunk: its registers -> LDS, the chunk two ahead into the same registers, arithmetic
+  // census bit 16: sub-phase marks of chunks 2 and 3 (slots 3-8, 9-14) instead of chunk ends
   auto process = [&](f32x4 (&v)[CC], int cb) {
+    [[maybe_unused]] const int ci = (cb - cs) / CC;
+#define WB_SUB(j) WB_MARKC((ci == 2 ? 3 : 9) + (j), WB_ABL(16) && (ci == 2 || ci == 3))
+    WB_SUB(0);
     lds_barrier();  // the previous chunk's readers are done
+    WB_SUB(1);
 #pragma unroll
     for (int c = 0; c < CC; ++c)  // planar [channel][window pixel]: conflict-free 16-B writes
       *reinterpret_cast<f32x4*>(dst + c * WN + sr * WS + 4 * sq) = v[c];
     lds_barrier();
-    WB_MARK(3 + min((cb - cs) / CC, 11));
-    if (cb + 2 * CC < ce) issue(v, cb + 2 * CC);
+    WB_MARKC(3 + min(ci, 11), !WB_ABL(16));
+    WB_SUB(2);
+    // unconditional: past the group's last channel the loads come back as zeros from the range
+    // check -- a skipped issue would leave the compiler's vmcnt count unsure at the next chunk,
+    // and it would then wait for the chunk after the one it needs as well
+    issue(v, cb + 2 * CC);
+    WB_SUB(3);
     // grad_x of tile pixel q, this half's channels of the chunk
     const int c0 = hf * HC;
     float acc[HC];
 #pragma unroll
     for (int c = 0; c < HC; ++c) acc[c] = 0.f;
     const int lenx = WB_ABL(4) ? 0 : len;
+    // the register entries without a branch: every LDS read of them is in flight at once
+    // (an `if (j < len)` per entry serialised one LDS round trip per entry); entries past the
+    // list are {0, 0} and leave the sum as it is (a select, not a multiply by a zero weight)
+    float gv[KE][HC];
 #pragma unroll
     for (int j = 0; j < KE; ++j)
-      if (j < lenx) {
-        const float w = __int_as_float(ent[j].y);
 #pragma unroll
-        for (int c = 0; c < HC; ++c) acc[c] += gs[(c0 + c) * WN + ent[j].x] * w;
+      for (int c = 0; c < HC; ++c) gv[j][c] = gs[(c0 + c) * WN + ent[j].x];
+#pragma unroll
+    for (int j = 0; j < KE; ++j) {
+      const float w = __int_as_float(ent[j].y);
+#pragma unroll
+      for (int c = 0; c < HC; ++c) {
+        const float s = acc[c] + gv[j][c] * w;
+        acc[c] = j < lenx ? s : acc[c];
       }
+    }
     for (int e = start + KE; e < start + lenx; ++e) {
       const int2 en = lent[e];
       const float w = __int_as_float(en.y);
@@ -332,6 +357,7 @@ __global__ __launch_bounds__(NT, 2) void warp_bwd_tile(Args a) {
                                ? ((unsigned)ch * plane + opix) * 4u : kOOB;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[c]), rsgx, (int)off, 0, 0);
     }
+    WB_SUB(4);
     if (own) {
       // grad_flow of p over this half's channels (x at the corners, masked outside the image)
       // (corners outside the window: zero here, added after the chunk loop)
@@ -347,10 +373,12 @@ __global__ __launch_bounds__(NT, 2) void warp_bwd_tile(Args a) {
         giy += go * ((r[2][c] - r[0][c]) * ob.wx0 + (r[3][c] - r[1][c]) * ob.wx1);
       }
     }
+    WB_SUB(5);
+#undef WB_SUB
   };
-  for (int cb = cs; cb < ce; cb += 2 * CC) {
+  for (int cb = cs; cb < ce; cb += 2 * CC) {  // an odd chunk count's last chunk is all zeros
     process(va, cb);
-    if (cb + CC < ce) process(vb, cb + CC);
+    process(vb, cb + CC);
   }
   // pixels with a corner outside the window (|flow| beyond the margin): their grad_flow over
   // this group's channels again from global memory, exactly (the loop above left such corners
