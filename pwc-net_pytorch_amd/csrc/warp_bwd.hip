@@ -533,11 +533,12 @@ extern "C" __attribute__((visibility("default"))) int pwc_debug_wbwd_census(void
                              sizeof(unsigned long long) * (size_t)n) == hipSuccess;
 }
 
-// The tile path's choice (warp_backward_tiles_f32): wide images by default; knob
-// warp_bwd_tiles = 0 never, 2 always.
+// The tile path's choice (warp_backward_tiles_f32): W >= 56 by default (config 5's l3 and l4;
+// at l3 23.4 vs 24.6 us for the list-gather path since round 5's branch-free chunk loop,
+// profiles/r05u_warp_bwd_tile_chunks.txt); knob warp_bwd_tiles = 0 never, 2 always.
 static bool tiles_wanted(int W) {
   const int mode = debug_knob("warp_bwd_tiles", 1);
-  return !(mode == 0 || (mode == 1 && W < 96));
+  return !(mode == 0 || (mode == 1 && W < 56));
 }
 
 // 0 whenever the tile path would decline, so the narrow levels pass no workspace
@@ -551,10 +552,10 @@ hipError_t warp_backward_tiles_f32(const void* x, const void* flow, const void* 
                                    void* gflow, int B, int C, int H, int W, void* ws,
                                    size_t ws_bytes, hipStream_t stream) {
   using namespace wbwd;
-  // measured (B=8 384x448, profiles/r03c_warp_bwd_tiles.txt): l4 (96 x 112) 34.9 -> 30.1 us;
-  // l3 equal, l2..l0 slower (the tile workgroup's list build + per-chunk barriers are a fixed
-  // latency that the multi-kernel path does not pay) -- wide images only by default; knob
-  // warp_bwd_tiles = 0 never, 2 always (tests)
+  // measured (B=8 384x448, profiles/r03c_warp_bwd_tiles.txt, r05u_*): l4 (96 x 112) 34.9 ->
+  // 26.4 us, l3 24.6 -> 23.4; l2..l0 slower (the tile workgroup's list build + per-chunk
+  // barriers are a fixed latency that the multi-kernel path does not pay) -- W >= 56 by
+  // default; knob warp_bwd_tiles = 0 never, 2 always (tests)
   if (!tiles_wanted(W)) return hipErrorNotSupported;
   Plan p;
   if (!plan(B, C, H, W, &p) || ws == nullptr || ws_bytes < p.bytes) return hipErrorNotSupported;

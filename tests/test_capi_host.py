@@ -83,7 +83,8 @@ def test_error_paths_return_zero_with_message():
     assert b"negative" in lib.pwc_last_error()
     assert lib.pwc_warp_backward_workspace_size(8, 32, 96, 112, 1) == 0      # fp16
     assert lib.pwc_warp_backward_workspace_size(8, 32, -96, 112, 0) == 0     # negative dim
-    assert lib.pwc_warp_backward_workspace_size(8, 64, 48, 56, 0) == 0       # l3: multi-kernel
+    assert lib.pwc_warp_backward_workspace_size(8, 96, 24, 28, 0) == 0       # l2: multi-kernel
+    assert lib.pwc_warp_backward_workspace_size(8, 64, 48, 56, 0) > 0        # l3: tile path
     assert lib.pwc_warp_backward_workspace_size(8, 32, 96, 112, 0) > 0       # l4: tile path
     with pytest.raises(RuntimeError, match="aborting"):
         _lib.check(0, "x")

@@ -291,7 +291,7 @@ def test_corr_backward_generic_low_precision(dtype):
     _check(g2, r2, dtype)
 
 
-@pytest.mark.parametrize("shape,what", [((16, 96, 28, 64), "warp_bwd_flow<8,4>"),
+@pytest.mark.parametrize("shape,what", [((16, 96, 28, 48), "warp_bwd_flow<8,4>"),
                                         ((1, 16, 48, 48), "warp_bwd_merged<16,16,6,8,2>")],
                          ids=["flow_ng4", "merged_ng2"])
 def test_warp_backward_reached_instantiations(shape, what):
