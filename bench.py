@@ -759,18 +759,19 @@ def cpu_baseline_port(shapes, B, seconds, threads):
                        f"C port oracle/pwc_oracle.c, {used} OpenMP threads, {el:.1f} s")
 
 
-def corr4_roofline(dev, dtype, B, shape, launches=100):
+def corr4_roofline(dev, dtype, B, shape, launches=100, cargs=None, what=None):
     """Secondary roofline line (labelled, not the headline): the north star's literal "d=4",
     Correlation(pad 4, k 1, md 4, s1 1, s2 1) -- 81 displacements -4..4 step 1, the same bytes
     and multiply-adds as model.py:24's Corr9 -- at the l4 shape, B pairs, each launch timed
     with hipExtLaunchKernel start/stop events (pwc_time_next_corr) on buffer sets rotated past
-    the Infinity Cache, launches back to back."""
+    the Infinity Cache, launches back to back.  `cargs` / `what`: another correlation config
+    and its label (config 4's synthetic 192x224x32 stress shape)."""
     from pwcnet_amd import _lib
     L = _lib.load()
     C, h, w = shape
     esz = 4 if dtype == torch.float32 else 2
-    P = [CORR4_ARGS[k] for k in ("pad_size", "kernel_size", "max_displacement", "stride1",
-                                 "stride2")]
+    P = [(cargs or CORR4_ARGS)[k] for k in ("pad_size", "kernel_size", "max_displacement",
+                                            "stride1", "stride2")]
     OC, Ho, Wo = _lib.corr_output_shape(h, w, *P)
     per = (2 * C * h * w + OC * Ho * Wo) * B * esz
     nsets = max(2, int(np.ceil(2 * 256 * 2 ** 20 / per)))
@@ -805,8 +806,10 @@ def corr4_roofline(dev, dtype, B, shape, launches=100):
     us = float(np.mean([a.elapsed_time(b) for a, b in evs])) * 1e3
     nbytes = corr_bytes_per_pair(C, h, w, esz) * B
     ach = nbytes / (us * 1e-6) / 1e9
-    return {"kernel": f"l4 Correlation(4, 1, 4, 1, 1) ({C}x{h}x{w}, B={B}, "
-                      f"{'fp32' if esz == 4 else 'fp16'}): the north star's literal d=4, "
+    kind = what or "l4 Correlation(4, 1, 4, 1, 1)"
+    why = "" if what else "the north star's literal d=4, "
+    return {"kernel": f"{kind} ({C}x{h}x{w}, B={B}, "
+                      f"{'fp32' if esz == 4 else 'fp16'}): {why}"
                       f"{launches} back-to-back launches, hipExtLaunchKernel start/stop events",
             "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes,
@@ -1199,6 +1202,12 @@ def main(argv=None):
     if rank == 0 and world == 1 and not cpu and not args.no_corr4:
         progress("Corr4 line")
         result["roofline_corr4"] = corr4_roofline(dev, dtype, B, shapes[-1])
+        if dtype == torch.float16:  # config 4's synthetic stress shape, labelled separately
+            progress("192x224x32 stress line")
+            result["stress_192x224x32"] = corr4_roofline(
+                dev, dtype, B, (32, 192, 224), cargs=CORR_ARGS,
+                what="synthetic stress shape (SURVEY.md §8: the north star's '192x224x32', no "
+                     "correlated level of the model) Correlation(9, 1, 9, 1, 2)")
     if rank == 0 and world == 1 and not cpu and not args.no_net_forward:
         progress("Net forward")
         result["net_forward"] = net_forward(dev, B, args.height, args.width,
