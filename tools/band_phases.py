@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--level", type=int, default=1)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--knobs", default="")
+    ap.add_argument("--chain", type=int, default=1)
     args = ap.parse_args()
     C, H, W = bench.level_shapes(384, 448)[args.level]
     B, dev = args.batch, torch.device("cuda:0")
@@ -49,14 +50,27 @@ def main():
         warp_corr_forward(x1, x2, fl, 9, 1, 9, 1, 2)
     torch.cuda.synchronize()
     lib.pwc_debug_band_reset()
-    warp_corr_forward(x1, x2, fl, 9, 1, 9, 1, 2)
+    # --chain N: the stamped launch is the last of N back to back (every workgroup rewrites its
+    # stamps), so it starts behind a running kernel as in the bench, not on an idle GPU
+    for _ in range(args.chain):
+        warp_corr_forward(x1, x2, fl, 9, 1, 9, 1, 2)
     torch.cuda.synchronize()
     buf = np.zeros(4096 * 8, np.uint64)
     assert lib.pwc_debug_band_times(buf.ctypes.data, buf.size) == 1
     _lib.set_debug("")
     t = buf.reshape(4096, 8).astype(np.int64)
-    t = t[t[:, 0] > 0]
+    blk = np.nonzero(t[:, 0] > 0)[0]
+    t = t[blk]
     t0 = t[:, 0].min()
+    ent = (t[:, 0] - t0) / 100.0
+    # entry against the block index (dispatch order) and by hardware XCD (blockIdx % 8)
+    order = np.argsort(blk)
+    q = len(blk) // 4
+    print(json.dumps({"entry_by_block_quarter_us": [round(float(np.median(ent[order[i * q:(i + 1) * q]])), 2)
+                                                     for i in range(4)],
+                      "entry_by_xcd_us": [round(float(np.median(ent[blk % 8 == x])), 2)
+                                          for x in range(8)],
+                      "entry_first_16_blocks_us": [round(float(v), 2) for v in ent[order[:16]]]}))
     out = dict(level=args.level, wgs=int(len(t)),
                entry_spread_us=round(float((t[:, 0].max() - t0) / 100), 2),
                last_end_us=round(float((t[:, 5].max() - t0) / 100), 2))
