@@ -862,13 +862,15 @@ def load_pmc_traffic(path):
         return None, None
 
 
-def live_pmc_traffic(B, H, W, dtype, timeout=150):
+def live_pmc_traffic(B, H, W, dtype, timeout=150, step=True):
     """HBM bytes per launch of the l4 correlation measured NOW: two rocprofv3 PMC passes (one
-    counter each: FETCH_SIZE, WRITE_SIZE; MI355X_MICROARCH.md's HBM recipe) over
-    tools/kbench.py's l4 correlation at this run's shape, as child processes in their own
-    process group (killed as a group on timeout).  FETCH_SIZE counts half the bytes of
-    16-B-per-lane streaming reads on gfx950 -> x2; both in KB.  Returns (bytes, note) or
-    (None, reason)."""
+    counter each: FETCH_SIZE, WRITE_SIZE; MI355X_MICROARCH.md's HBM recipe), as child processes
+    in their own process group (killed as a group on timeout).  step=True: over this bench's
+    own dependency-order step (a short `bench.py --no-pmc` child at this run's shape: the l4
+    correlation right after its warp, on the rotating buffer sets of the timed region; the l4
+    dispatches picked by their C = 32 geometry); step=False: over tools/kbench.py's l4
+    correlation alone.  FETCH_SIZE counts half the bytes of 16-B-per-lane streaming reads on
+    gfx950 -> x2; both in KB.  Returns (bytes, note) or (None, reason)."""
     import csv
     import shutil
     import signal
@@ -878,13 +880,20 @@ def live_pmc_traffic(B, H, W, dtype, timeout=150):
         return None, "rocprofv3 not found"
     kb = {}
     tmp = tempfile.mkdtemp(prefix="pwc_pmc_", dir="/tmp")
+    shape = ["--batch", str(B), "--height", str(H), "--width", str(W), "--dtype", dtype]
+    if step:
+        child = [os.path.join(ROOT, "bench.py"), "--steps", "20", "--warmup", "20", "--no-pmc",
+                 "--no-cpu-baseline", "--no-net-forward", "--no-corr4", "--grouped-mode",
+                 "off"] + shape
+        pick = L4_KERNEL_RE + r".*Geo<32,"
+    else:
+        child = [os.path.join(ROOT, "tools", "kbench.py"), "--levels", "4", "--ops", "corr",
+                 "--iters", "20"] + shape
+        pick = L4_KERNEL_RE
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         out = os.path.join(tmp, ctr)
         cmd = [prof, "--pmc", ctr, "--kernel-include-regex", L4_KERNEL_RE, "-d", out, "-o",
-               "run", "--output-format", "csv", "--", sys.executable,
-               os.path.join(ROOT, "tools", "kbench.py"), "--levels", "4", "--ops", "corr",
-               "--iters", "20", "--batch", str(B), "--height", str(H), "--width", str(W),
-               "--dtype", dtype]
+               "run", "--output-format", "csv", "--", sys.executable] + child
         env = dict(os.environ, TMPDIR="/tmp")
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
                              stderr=subprocess.DEVNULL, start_new_session=True)
@@ -899,16 +908,20 @@ def live_pmc_traffic(B, H, W, dtype, timeout=150):
             for f in files:
                 if f.endswith("counter_collection.csv"):
                     for r in csv.DictReader(open(os.path.join(root, f))):
-                        if re.search(L4_KERNEL_RE, r["Kernel_Name"]):
+                        if re.search(pick, r["Kernel_Name"]):
                             vals.append(float(r["Counter_Value"]))
         if p.returncode != 0 or not vals:
-            return None, f"rocprofv3 --pmc {ctr} failed (rc {p.returncode})"
+            return None, f"rocprofv3 --pmc {ctr} failed (rc {p.returncode}, {len(vals)} rows)"
         kb[ctr] = sum(vals) / len(vals)
+        kb["n"] = len(vals)
     shutil.rmtree(tmp, ignore_errors=True)
     rd, wr = kb["FETCH_SIZE"] * 1024 * 2, kb["WRITE_SIZE"] * 1024
-    return int(rd + wr), (f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
-                          f"tools/kbench.py --levels 4 in this run (reads {int(rd)} B with the "
-                          f"gfx950 x2 FETCH_SIZE correction, writes {int(wr)} B per launch)")
+    where = (f"this bench's dependency-order step (a bench.py child at the same shape, the "
+             f"{kb['n']} l4 correlation dispatches of 20 timed + 20 warm-up steps and its checks)"
+             if step else "tools/kbench.py --levels 4")
+    return int(rd + wr), (f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over {where} "
+                          f"in this run (reads {int(rd)} B with the gfx950 x2 FETCH_SIZE "
+                          f"correction, writes {int(wr)} B per launch)")
 
 
 # ---------------------------------------------------------------------------------------
@@ -1181,6 +1194,11 @@ def main(argv=None):
         if not args.no_pmc and rank == 0 and world == 1:
             progress("live PMC passes")
             traffic, tsrc = live_pmc_traffic(B, args.height, args.width, args.dtype)
+            if traffic is None:  # the isolated kernel instead
+                why = tsrc
+                traffic, tsrc = live_pmc_traffic(B, args.height, args.width, args.dtype,
+                                                 step=False)
+                tsrc = f"{tsrc} (in-step passes not taken: {why})"
         if traffic is None and args.dtype == "fp32" and (B, args.height, args.width) == (
                 8, 384, 448):
             why = tsrc
