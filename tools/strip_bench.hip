@@ -60,6 +60,8 @@ using G7 = pwc::strip::Geo<32, 12, 56, 2, 4, 1>;
 using G8 = pwc::strip::Geo<32, 12, 56, 2, 4, 2>;
 using G9 = pwc::strip::Geo<32, 6, 56, 1, 2, 2>;
 using G10 = pwc::strip::GeoF;
+using G11 = pwc::strip::Geo<32, 6, 112, 2, 3, 1, true>;     // 2 steps of 3 rows, 12 compute waves
+using G12 = pwc::strip::Geo<32, 6, 112, 2, 1, 1, true, 4>;  // 6 steps of 1 row, channel quarters
 static int g_geo = 10;
 template <class F>
 static auto with_geo(F&& f) {
@@ -70,6 +72,8 @@ static auto with_geo(F&& f) {
     case 8: return f(G8{});
     case 9: return f(G9{});
     case 10: return f(G10{});
+    case 11: return f(G11{});
+    case 12: return f(G12{});
     case 5: return f(G5{});
     default: return f(G10{});
   }
