@@ -65,6 +65,21 @@ def test_stress_192x224x32_fp16():
     _close_rel(_np(out), O.corr_forward(_np(a), _np(b), 9, 1, 9, 1, 2), 2e-3)
 
 
+def test_stress_192x224x32_fp16_b16_matrix_cores():
+    """The stress shape at the batch bench.py's `stress_192x224x32` line times (B = 16): the
+    matrix-core strip kernel (two column strips, 128 + 96 px, the second one partial); images 0
+    and 15 against the oracle."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import corr_forward
+    assert _lib.corr_forward_plan(16, 32, 192, 224, 9, 1, 9, 1, 2, 1) == "mstrip16"
+    rng = np.random.default_rng(79)
+    a, b = _h(rng, 16, 32, 192, 224), _h(rng, 16, 32, 192, 224)
+    out = corr_forward(a, b, 9, 1, 9, 1, 2)
+    torch.cuda.synchronize()
+    pick = [0, 15]
+    _close_rel(_np(out[pick]), O.corr_forward(_np(a[pick]), _np(b[pick]), 9, 1, 9, 1, 2), 2e-3)
+
+
 def test_stress_192x224x32_fp32():
     from pwcnet_amd.ops import corr_forward
     rng = np.random.default_rng(78)
