@@ -153,7 +153,7 @@ __global__ void corr_bwd_generic(const T* __restrict__ in1, const T* __restrict_
   }
 }
 
-// corr_bwd_strip.hip: model.py:24's configuration at the strip-sized levels (config 5 l3/l4),
+// corr_bwd_strip.hip: model.py:24's configuration at the strip-sized levels (config 5 l2/l3/l4),
 // fp32; it declines everything else.
 hipError_t corr_backward_strip_f32(const void* in1, const void* in2, const void* gout, void* g1,
                                    void* g2, int B, int C, int H, int W, float divisor,

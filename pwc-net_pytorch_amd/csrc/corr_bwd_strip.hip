@@ -1,6 +1,6 @@
 // corr_bwd_strip.hip — correlation backward of model.py:24's configuration (pad == md in {8, 9},
 // k 1, s1 1, s2 2: 81 displacement channels, /C) for the strip-sized fp32 levels (config 5's
-// l3 / l4), both gradients in one launch, no atomics, no partial sums through LDS or HBM.
+// l2 / l3 / l4), both gradients in one launch, no atomics, no partial sums through LDS or HBM.
 //
 //   g1[n,c,y,x]   = sum_t gO[n,t,y,x] * f2[n,c,y+2tj-8,x+2ti-8] / C            (cu:108-198)
 //   g2[n,c,y',x'] = sum_t gO[n,t,y'-2tj+8,x'-2ti+8] * f1[n,c,y'-2tj+8,x'-2ti+8] / C
@@ -407,6 +407,13 @@ using GeoB4 = Geo<PWC_BWD_GEO4>;
 #define PWC_BWD_GEO3 64, 3, 14, 8
 #endif
 using GeoB3 = Geo<PWC_BWD_GEO3>;
+// config 5 l2 (C = 96, W = 28): 2-row bands (192 workgroups), 8 channels per lane -- in the
+// training step 12.0 -> 11.2 us against corr_bwd_rows (3-row bands 13.0, 1-row 14.5, 4
+// channels per lane 11.4; profiles/r05z_bwd_strip_l2.txt)
+#ifndef PWC_BWD_GEO2
+#define PWC_BWD_GEO2 96, 2, 7, 8
+#endif
+using GeoB2 = Geo<PWC_BWD_GEO2>;
 
 }  // namespace bstrip
 
@@ -423,6 +430,9 @@ static int bwd_strip_plan(const void* in1, const void* in2, const void* gout, co
   if ((size_t)81 * H * W * 4 >= 0x7ffffff0ull || (size_t)C * H * W * 4 >= 0x7ffffff0ull) return 0;
   if (C == 32 && W == 4 * bstrip::GeoB4::NSEG && C % bstrip::GeoB4::CW == 0) return 4;
   if (C == 64 && W == 4 * bstrip::GeoB3::NSEG && C % bstrip::GeoB3::CW == 0) return 3;
+  if (C == 96 && W == 4 * bstrip::GeoB2::NSEG && C % bstrip::GeoB2::CW == 0 &&
+      debug_knob("bwd_strip_l2", 1) != 0)
+    return 2;
   return 0;
 }
 
@@ -445,6 +455,8 @@ hipError_t corr_backward_strip_f32(const void* in1, const void* in2, const void*
       return bstrip::launch<bstrip::GeoB4>(a, stream);
     case 3:
       return bstrip::launch<bstrip::GeoB3>(a, stream);
+    case 2:
+      return bstrip::launch<bstrip::GeoB2>(a, stream);
     default:
       return hipErrorNotSupported;
   }

@@ -249,16 +249,17 @@ def test_corr_forward_plan_routes_and_declines():
 
 
 def test_corr_backward_plan_routes_and_declines():
-    """pwc_corr_backward_plan: config 5's l4 / l3 backward reach the displacement-row strip
-    kernel, the other levels the row-band kernel, other configurations and dtypes the stencil
-    kernels; rejected arguments -1."""
+    """pwc_corr_backward_plan: config 5's l4 / l3 / l2 backward reach the displacement-row
+    strip kernel, the other levels the row-band kernel, other configurations and dtypes the
+    stencil kernels; rejected arguments -1."""
     from pwcnet_amd import _lib
     plan = _lib.corr_backward_plan
     c9 = (9, 1, 9, 1, 2)
     assert plan(8, 32, 96, 112, *c9) == "strip"   # config 5 l4
     assert plan(8, 64, 48, 56, *c9) == "strip"    # config 5 l3
     assert plan(1, 32, 7, 112, *c9) == "strip"    # a band taller than the image
-    assert plan(8, 96, 24, 28, *c9) == "rows"     # l2
+    assert plan(8, 96, 24, 28, *c9) == "strip"    # l2
+    assert plan(8, 96, 24, 30, *c9) == "rows"     # l2-like, another width
     assert plan(8, 192, 6, 7, *c9) == "rows"      # l0
     assert plan(8, 32, 96, 112, 8, 1, 8, 1, 2) == "strip"  # pad = md = 8
     assert plan(8, 32, 96, 112, 4, 1, 4, 1, 1) == "other"  # Corr4

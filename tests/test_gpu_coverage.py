@@ -413,11 +413,12 @@ def test_warp_fp16_alignment(case):
         assert torch.equal(out, warp_forward(x, f))
 
 
-# corr_bwd_strip.hip (config 5's l4 / l3 backward): whole batches at the geometries' shapes, odd
-# heights (the odd-row parity has a band fewer / a short band), a height below one band, batch
-# 1; against the oracle, and repeatable bit for bit.
+# corr_bwd_strip.hip (config 5's l4 / l3 / l2 backward): whole batches at the geometries' shapes,
+# odd heights (the odd-row parity has a band fewer / a short band), a height below one band,
+# batch 1; against the oracle, and repeatable bit for bit.
 BWD_STRIP = [(1, 32, 96, 112), (2, 32, 95, 112), (1, 32, 6, 112), (1, 32, 14, 112),
-             (2, 64, 48, 56), (1, 64, 47, 56), (3, 64, 10, 56)]
+             (2, 64, 48, 56), (1, 64, 47, 56), (3, 64, 10, 56),
+             (2, 96, 24, 28), (1, 96, 23, 28), (1, 96, 3, 28)]
 
 
 @pytest.mark.parametrize("shape", BWD_STRIP, ids=lambda s: "x".join(map(str, s)))
@@ -439,13 +440,14 @@ def test_corr_backward_strip_vs_oracle(shape):
     assert torch.equal(g1, h1) and torch.equal(g2, h2)
 
 
-@pytest.mark.parametrize("level", [3, 4])
+@pytest.mark.parametrize("level", [2, 3, 4])
 def test_corr_backward_strip_full_batch_vs_rows(level):
-    """BASELINE config 5 (B = 8, 384x448) at l3 / l4: the strip backward against the row-band
-    kernel (knob bwd_strip=0) on the same inputs, within fp32 summation-order differences."""
+    """BASELINE config 5 (B = 8, 384x448) at l2 / l3 / l4: the strip backward against the
+    row-band kernel (knob bwd_strip=0) on the same inputs, within fp32 summation-order
+    differences."""
     from pwcnet_amd import _lib
     from pwcnet_amd.ops import corr_backward
-    C, H, W = {3: (64, 48, 56), 4: (32, 96, 112)}[level]
+    C, H, W = {2: (96, 24, 28), 3: (64, 48, 56), 4: (32, 96, 112)}[level]
     shape = (8, C, H, W)
     a, _ = _rand(shape, torch.float32, "fba", level)
     b, _ = _rand(shape, torch.float32, "fbb", level)
