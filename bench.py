@@ -151,7 +151,7 @@ def parse_args(argv=None):
                     help="grouped mode: the unfused levels' warps (l2, l3, l4) as one pwc_warp_forward_group "
                          "launch ahead of their correlations (independent inputs); off = one "
                          "warp call per level")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02l_l4corr_pmc.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05_l4corr_pmc.json"),
                     help="committed PMC summary used when the live passes cannot run")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 PMC passes for roofline.traffic")
