@@ -267,3 +267,33 @@ def test_corr_backward_plan_routes_and_declines():
     assert plan(8, 32, 96, 112, *c9, ptrs=(0x1000, 0x2000, 0x3004, 0x4000, 0x5000)) == "rows"
     assert plan(8, 32, 96, 112, 9, 1, 9, 2, 2) == -1       # stride1 != 1: undefined backward
     assert plan(8, 32, 96, 112, *c9, dtype=5) == -1
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No silent fallback: with the HIP library absent, loading it raises HipLibraryMissing, and
+    an op on CPU tensors raises too (the product path has no CPU or oracle route)."""
+    import subprocess
+    import sys
+    code = (
+        "import torch, pwcnet_amd\n"
+        "from pwcnet_amd import _lib\n"
+        "from pwcnet_amd.ops import corr_forward, warp_forward\n"
+        "a, f = torch.zeros(1, 4, 6, 7), torch.zeros(1, 2, 6, 7)\n"
+        "try:\n"
+        "    _lib.load()\n"
+        "except _lib.HipLibraryMissing as e:\n"
+        "    print('missing:', e)\n"
+        "for fn in (lambda: corr_forward(a, a, 9, 1, 9, 1, 2), lambda: warp_forward(a, f)):\n"
+        "    try:\n"
+        "        fn()\n"
+        "    except RuntimeError as e:\n"
+        "        print('raised:', e)\n")
+    env = dict(os.environ, PWC_HOTPATH_LIB=str(tmp_path / "absent.so"))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "pwc-net_pytorch_amd"), root,
+                                         env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "missing:" in r.stdout and "not built" in r.stdout, r.stdout
+    assert r.stdout.count("raised:") == 2 and "HIP devices only" in r.stdout, r.stdout
