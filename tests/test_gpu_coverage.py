@@ -462,3 +462,29 @@ def test_corr_backward_strip_full_batch_vs_rows(level):
     for x, y in ((g1, r1), (g2, r2)):
         err = float((x - y).abs().max()) / float(y.abs().max())
         assert err < 1e-5, err
+
+
+def test_missing_library_fails_loudly_on_gpu(tmp_path):
+    """On the GPU too: with the HIP library absent, an op on device tensors raises
+    HipLibraryMissing instead of running anything else (no eager / oracle fallback)."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import torch, pwcnet_amd\n"
+        "from pwcnet_amd import _lib\n"
+        "from pwcnet_amd.ops import corr_forward, warp_forward\n"
+        "a, f = torch.zeros(1, 4, 6, 8, device='cuda'), torch.zeros(1, 2, 6, 8, device='cuda')\n"
+        "for fn in (lambda: corr_forward(a, a, 9, 1, 9, 1, 2), lambda: warp_forward(a, f)):\n"
+        "    try:\n"
+        "        fn()\n"
+        "    except _lib.HipLibraryMissing as e:\n"
+        "        print('raised:', e)\n")
+    env = dict(os.environ, PWC_HOTPATH_LIB=str(tmp_path / "absent.so"))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "pwc-net_pytorch_amd"), root,
+                                         env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("raised:") == 2 and "not built" in r.stdout, r.stdout
