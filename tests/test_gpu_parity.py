@@ -577,3 +577,53 @@ def test_corr_forward_with_and_without_workspace(case):
             ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
             ctypes.c_void_p(outs[0].data_ptr()), B, C, H, W, 9, 1, 9, 1, 2, 1, 0,
             ctypes.c_void_p(ws.data_ptr()), nws - 4, stream), "t")
+
+
+@pytest.mark.parametrize("cfg", [(9, 1, 9, 1, 2), (4, 1, 4, 1, 1)], ids=["corr9", "corr4"])
+@pytest.mark.parametrize("shape", [(1, 1, 1, 1), (2, 3, 1, 9), (1, 5, 9, 1), (3, 1, 5, 5),
+                                   (1, 2, 2, 3), (0, 4, 6, 7)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_correlation_degenerate_shapes(shape, cfg):
+    """Single-pixel, single-row / single-column images, one channel and an empty batch through
+    the default dispatch, forward and backward, against the oracle (every displacement but
+    (0, 0) of a 1 x 1 image falls in the zero padding)."""
+    from pwcnet_amd.ops import corr_backward, corr_forward
+    rng = np.random.default_rng(_seed("degenerate", shape, cfg))
+    a, b = _rand(rng, *shape), _rand(rng, *shape)
+    out = corr_forward(_t(a), _t(b), *cfg)
+    torch.cuda.synchronize()
+    assert tuple(out.shape) == (shape[0], 81, shape[2], shape[3])
+    if shape[0] == 0:
+        return
+    np.testing.assert_allclose(_np(out), O.corr_forward(a, b, *cfg), rtol=1e-5, atol=1e-6)
+    g = _rand(rng, *out.shape)
+    g1, g2 = corr_backward(_t(a), _t(b), _t(g), *cfg)
+    torch.cuda.synchronize()
+    r1, r2 = O.corr_backward(a, b, g, *cfg)
+    np.testing.assert_allclose(_np(g1), r1, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(_np(g2), r2, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 2, 2), (2, 3, 2, 9), (1, 4, 9, 2), (0, 4, 6, 7)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_warp_degenerate_shapes(shape):
+    """2-pixel-wide / 2-row images (the smallest the reference's (size - 1) / 2 normalisation
+    allows), one channel and an empty batch: warp forward and backward against the oracle,
+    flows reaching past every border."""
+    from pwcnet_amd.ops import warp_backward, warp_forward
+    B, C, H, W = shape
+    rng = np.random.default_rng(_seed("warp-degenerate", shape))
+    x = _rand(rng, *shape)
+    f = (rng.standard_normal((B, 2, H, W)) * 1.5).astype(np.float32)
+    out = warp_forward(_t(x), _t(f))
+    torch.cuda.synchronize()
+    assert tuple(out.shape) == shape
+    if B == 0:
+        return
+    np.testing.assert_allclose(_np(out), O.warp_forward(x, f), rtol=1e-5, atol=1e-6)
+    g = _rand(rng, *shape)
+    gx, gf = warp_backward(_t(x), _t(f), _t(g))
+    torch.cuda.synchronize()
+    rx, rf = O.warp_backward(x, f, g)
+    np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4)
