@@ -627,3 +627,46 @@ def test_warp_degenerate_shapes(shape):
     rx, rf = O.warp_backward(x, f, g)
     np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("level", [0, 1, 2, 3, 4])
+def test_full_size_homogeneity_config2(level):
+    """Config 2 (B = 8, 384x448) at every level, fp32: corr(2a, b) == 2 corr(a, b) and
+    warp(2x, f) == 2 warp(x, f) bit for bit (a power-of-two scale is exact through every product,
+    sum and the /C) -- a size-independent check of the default kernels at full size."""
+    from bench import level_shapes
+    from pwcnet_amd.ops import corr_forward, warp_forward
+    C, H, W = level_shapes(384, 448)[level]
+    rng = np.random.default_rng(_seed("homog", level))
+    a, b = _t(_rand(rng, 8, C, H, W)), _t(_rand(rng, 8, C, H, W))
+    f = _t((rng.standard_normal((8, 2, H, W)) * 2).astype(np.float32))
+    assert torch.equal(corr_forward(2 * a, b, 9, 1, 9, 1, 2), 2 * corr_forward(a, b, 9, 1, 9, 1, 2))
+    assert torch.equal(warp_forward(2 * a, f), 2 * warp_forward(a, f))
+
+
+@pytest.mark.parametrize("level", [2, 3, 4])
+def test_full_size_adjoint_config5(level):
+    """Config 5 (B = 8, 384x448) at l2-l4: the backward kernels are the adjoints of the forward
+    ones -- <corr(a, b), g> = <a, dL/da> = <b, dL/db> and <warp(x, f), g> = <x, dL/dx> (both
+    maps are linear in the argument), in float64 sums over the full tensors."""
+    from bench import level_shapes
+    from pwcnet_amd.ops import corr_backward, corr_forward, warp_backward, warp_forward
+    C, H, W = level_shapes(384, 448)[level]
+    rng = np.random.default_rng(_seed("adjoint", level))
+    a, b = _t(_rand(rng, 8, C, H, W)), _t(_rand(rng, 8, C, H, W))
+    g = _t(_rand(rng, 8, 81, H, W))
+    f = _t((rng.standard_normal((8, 2, H, W)) * 2).astype(np.float32))
+    gw = _t(_rand(rng, 8, C, H, W))
+    out = corr_forward(a, b, 9, 1, 9, 1, 2)
+    g1, g2 = corr_backward(a, b, g, 9, 1, 9, 1, 2)
+    w = warp_forward(a, f)
+    gx, _ = warp_backward(a, f, gw)
+    torch.cuda.synchronize()
+
+    def dot(x, y):
+        return float((x.double() * y.double()).sum())
+    lhs = dot(out, g)
+    for rhs in (dot(a, g1), dot(b, g2)):
+        assert abs(lhs - rhs) <= 1e-5 * (abs(lhs) + float((out.double().abs() * g.double().abs()).sum())), (lhs, rhs)
+    lw, rw = dot(w, gw), dot(a, gx)
+    assert abs(lw - rw) <= 1e-5 * float((w.double().abs() * gw.double().abs()).sum()), (lw, rw)
