@@ -670,3 +670,36 @@ def test_full_size_adjoint_config5(level):
         assert abs(lhs - rhs) <= 1e-5 * (abs(lhs) + float((out.double().abs() * g.double().abs()).sum())), (lhs, rhs)
     lw, rw = dot(w, gw), dot(a, gx)
     assert abs(lw - rw) <= 1e-5 * float((w.double().abs() * gw.double().abs()).sum()), (lw, rw)
+
+
+@pytest.mark.parametrize("level", [0, 1, 2, 3, 4])
+def test_full_size_homogeneity_config4_and_fused(level):
+    """Config 4 (B = 16, 448x1024, fp16 storage) at every level: corr(2a, b) == 2 corr(a, b)
+    and warp(2x, f) == 2 warp(x, f) bit for bit wherever the output is a normal fp16 number
+    (fp32 arithmetic, one fp16 rounding of an exactly doubled value; where the undoubled output
+    is subnormal its rounding quantum does not scale, so there the two may differ by one 2^-24
+    step; inputs carry no subnormals); and the fused warp + correlation (model.py:80-83) of
+    config 2's level in fp32 bit for bit."""
+    from bench import level_shapes
+    from pwcnet_amd.ops import corr_forward, warp_corr_forward, warp_forward
+    C, H, W = level_shapes(448, 1024)[level]
+    rng = np.random.default_rng(_seed("homog16", level))
+    def no_subnormals(v):  # inputs without fp16 subnormals: the check is about output rounding
+        return np.where(np.abs(v) < 2.0 ** -12, 0.0, v).astype(np.float32)
+    a = _t(no_subnormals(_rand(rng, 16, C, H, W)), torch.float16)
+    b = _t(no_subnormals(_rand(rng, 16, C, H, W)), torch.float16)
+    f = _t((rng.standard_normal((16, 2, H, W)) * 2).astype(np.float32), torch.float16)
+
+    def same_but_subnormals(x, y):
+        x, y = x.float(), y.float()
+        normal = y.abs() > 2.0 ** -13  # y = 2 * (a normal fp16 value above the smallest)
+        assert torch.equal(x[normal], y[normal])
+        assert float((x - y).abs().max()) <= 2.0 ** -24
+    same_but_subnormals(corr_forward(2 * a, b, 9, 1, 9, 1, 2), 2 * corr_forward(a, b, 9, 1, 9, 1, 2))
+    same_but_subnormals(warp_forward(2 * a, f), 2 * warp_forward(a, f))
+    C2, H2, W2 = level_shapes(384, 448)[level]
+    x1, x2 = _t(_rand(rng, 8, C2, H2, W2)), _t(_rand(rng, 8, C2, H2, W2))
+    f2 = _t((rng.standard_normal((8, 2, H2, W2)) * 2).astype(np.float32))
+    c1, w1 = warp_corr_forward(x1, 2 * x2, f2, 9, 1, 9, 1, 2)
+    c0, w0 = warp_corr_forward(x1, x2, f2, 9, 1, 9, 1, 2)
+    assert torch.equal(c1, 2 * c0) and torch.equal(w1, 2 * w0)
