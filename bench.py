@@ -686,7 +686,14 @@ def cpu_baseline_torch(shapes, batches=(8, 1), warmup=3, runs=5, max_seconds=12.
                                   median_ms=round(med * 1e3, 2), runs=len(times)))
     finally:
         torch.set_num_threads(prev)
-    b8 = max((l for l in lines if l["B"] == max(batches)), key=lambda l: l["value"])
+    # the main batch's line; when its first pass overran the budget (skipped), the best line
+    # timed at all, or no value -- the GPU line must not be lost to the CPU baseline
+    main = [l for l in lines if l["B"] == max(batches)] or lines
+    if not main:
+        return dict(value=None, unit="image-pairs/s", cores=usable, kind="port",
+                    usable_cpus=usable, lines=lines, skipped=skipped, **topo,
+                    sample="every CPU-baseline line overran its time budget (see 'skipped')")
+    b8 = max(main, key=lambda l: l["value"])
     return dict(value=b8["value"], unit="image-pairs/s", cores=b8["threads"], kind="port",
                 usable_cpus=usable, lines=lines, skipped=skipped, **topo,
                 sample=f"B={b8['B']} synthetic pairs, median of {b8['runs']} passes after "
@@ -1233,7 +1240,8 @@ def main(argv=None):
     if rank == 0 and world == 1 and not cpu and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_torch(shapes, batches=(B, 1),
                                                     max_seconds=args.cpu_seconds)
-        result["cpu_baseline"]["speedup"] = round(value / result["cpu_baseline"]["value"], 1)
+        cpu_v = result["cpu_baseline"]["value"]
+        result["cpu_baseline"]["speedup"] = round(value / cpu_v, 1) if cpu_v else None
         thr = result["cpu_baseline"]["cores"]
         progress(f"C port baseline ({thr} threads)")
         result["cpu_baseline_port"] = cpu_baseline_port(shapes, B, args.cpu_seconds / 2, thr)

@@ -8,7 +8,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/pwc_hotpath.h"
@@ -71,6 +74,20 @@ int debug_knob(const char* name, int def) {
     pos = end + 1;
   }
   return def;
+}
+
+hipError_t lds_limit(const void* kernel, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> done;  // (kernel, device) -> bytes set
+  std::lock_guard<std::mutex> lock(mu);
+  const auto it = done.find({kernel, dev});
+  if (it != done.end() && it->second >= bytes) return hipSuccess;
+  e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done[{kernel, dev}] = bytes;
+  return e;
 }
 
 // output epilogue of the next correlation launch of this thread (pwc_corr_forward_into)

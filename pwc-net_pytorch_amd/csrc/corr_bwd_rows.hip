@@ -433,13 +433,10 @@ hipError_t corr_backward_rows_f32(const void* in1, const void* in2, const void* 
   const unsigned units = (unsigned)(B * 2 * g.nb);
 #define PWC_BWD(V, CTT, M)                                                                     \
   if (vec == V && CT == CTT && ml <= M) {                                                      \
-    static bool attr = false;                                                                  \
-    if (!attr) {                                                                               \
-      hipError_t e = hipFuncSetAttribute(                                                      \
-          reinterpret_cast<const void*>(&corr_bwd_rows<V, CTT, M, NT>),                        \
-          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                             \
+    {  /* > 64 KiB dynamic LDS, once per device (capi.hip) */                                  \
+      const hipError_t e = lds_limit(                                                          \
+          reinterpret_cast<const void*>(&corr_bwd_rows<V, CTT, M, NT>), 160 * 1024);           \
       if (e != hipSuccess) return e;                                                           \
-      attr = true;                                                                             \
     }                                                                                          \
     hipLaunchKernelGGL((corr_bwd_rows<V, CTT, M, NT>), dim3(units, nsl, 2), dim3(NT), lds,     \
                        stream, (const float*)in1, (const float*)in2, (const float*)gout,       \

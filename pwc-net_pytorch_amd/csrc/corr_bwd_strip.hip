@@ -171,7 +171,6 @@ struct Args {
   float* g1;
   float* g2;
   int C, H, W, nb, ns, B;
-  float inv_divisor, divisor;
 };
 
 template <class G, int GRAD>
@@ -338,9 +337,12 @@ __device__ __forceinline__ void body(const Args& a, int n, int p, int band, int 
 #pragma unroll
     for (int j = 0; j < G::CS; ++j) {
       f32x4 v;
+      // / C, the geometry's compile-time channel count (the launcher checks divisor == C):
+      // an exact 2^-k multiply, or the reference's fp32 division (cu:196, 288) for C = 96 --
+      // as in the forward strips, no runtime select between the stores
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        v[e] = a.inv_divisor != 0.f ? acc[j][e] * a.inv_divisor : acc[j][e] / a.divisor;
+        v[e] = (G::CW & (G::CW - 1)) == 0 ? acc[j][e] * (1.f / G::CW) : acc[j][e] / (float)G::CW;
       st_out4(gimg + (size_t)j * H * W, v);
     }
   }
@@ -382,13 +384,10 @@ static hipError_t launch(const Args& a0, hipStream_t stream) {
   const long long nblk = 2LL * a.B * 2 * a.nb * a.ns;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_bwd_strip<G>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             G::LDS_BYTES + CENSUS_EXTRA);
+  {  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
+    const hipError_t e =
+        lds_limit(reinterpret_cast<const void*>(&corr_bwd_strip<G>), G::LDS_BYTES + CENSUS_EXTRA);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   hipLaunchKernelGGL((corr_bwd_strip<G>), dim3((unsigned)nblk), dim3(G::THREADS),
                      G::LDS_BYTES + CENSUS_EXTRA,
@@ -428,9 +427,10 @@ static int bwd_strip_plan(const void* in1, const void* in2, const void* gout, co
       (uintptr_t)g1 % 16 || (uintptr_t)g2 % 16)
     return 0;
   if ((size_t)81 * H * W * 4 >= 0x7ffffff0ull || (size_t)C * H * W * 4 >= 0x7ffffff0ull) return 0;
-  if (C == 32 && W == 4 * bstrip::GeoB4::NSEG && C % bstrip::GeoB4::CW == 0) return 4;
-  if (C == 64 && W == 4 * bstrip::GeoB3::NSEG && C % bstrip::GeoB3::CW == 0) return 3;
-  if (C == 96 && W == 4 * bstrip::GeoB2::NSEG && C % bstrip::GeoB2::CW == 0 &&
+  // every geometry stages all C channels in one workgroup (CW = C: the kernel divides by CW)
+  if (C == 32 && W == 4 * bstrip::GeoB4::NSEG && C == bstrip::GeoB4::CW) return 4;
+  if (C == 64 && W == 4 * bstrip::GeoB3::NSEG && C == bstrip::GeoB3::CW) return 3;
+  if (C == 96 && W == 4 * bstrip::GeoB2::NSEG && C == bstrip::GeoB2::CW &&
       debug_knob("bwd_strip_l2", 1) != 0)
     return 2;
   return 0;
@@ -445,11 +445,11 @@ hipError_t corr_backward_strip_f32(const void* in1, const void* in2, const void*
                                    void* g2, int B, int C, int H, int W, float divisor,
                                    hipStream_t stream) {
   const int plan = bwd_strip_plan(in1, in2, gout, g1, g2, B, C, H, W);
-  if (plan == 0) return hipErrorNotSupported;
-  int ex;
-  const float m = std::frexp(divisor, &ex);
+  // the kernels divide by their compile-time C: Correlation's divisor k^2 C with k = 1 (any other
+  // divisor goes on to corr_bwd_rows.hip)
+  if (plan == 0 || divisor != (float)C) return hipErrorNotSupported;
   bstrip::Args a{(const float*)in1, (const float*)in2, (const float*)gout, (float*)g1, (float*)g2,
-                 C, H, W, 0, 0, B, m == 0.5f ? std::ldexp(1.f, 1 - ex) : 0.f, divisor};
+                 C, H, W, 0, 0, B};
   switch (plan) {
     case 4:
       return bstrip::launch<bstrip::GeoB4>(a, stream);

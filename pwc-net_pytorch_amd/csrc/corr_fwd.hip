@@ -427,13 +427,10 @@ static hipError_t launch_tiled(const void* in1, const void* in2, void* out, int 
   const bool vec_ok = (W % 4 == 0) && (Wo % 4 == 0) && (off % 4 == 0) && (G::HALO % 4 == 0) &&
                       ((uintptr_t)in1 % align == 0) && ((uintptr_t)in2 % align == 0) &&
                       ((uintptr_t)out % 16 == 0);
-  static bool attr_set = false;  // one-time opt-in for > 64 KiB dynamic LDS
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_tiled<G, T>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       G::LDS_BYTES);
+  {  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
+    const hipError_t e =
+        lds_limit(reinterpret_cast<const void*>(&corr_fwd_tiled<G, T>), G::LDS_BYTES);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   const int nchunks = (C + G::CC - 1) / G::CC;
   int nsplit = partial ? corr_pick_splits(nblk, nchunks, max_splits) : 1;
@@ -570,9 +567,14 @@ hipError_t corr_forward_t(const void* in1, const void* in2, void* out, int B, in
                        ? corr_forward_path(in1, in2, out, B, C, H, W, pad, k, md, s1, s2, layout,
                                            kHalf ? 1 : 0)
                        : kPathOther;
-  if (path == kPathStream)
-    return corr_forward_stream(in1, in2, out, B, C, H, W, s2, kHalf ? 1 : 0, layout, divisor,
-                               stream);
+  if (path == kPathStream) {
+    const hipError_t e = corr_forward_stream(in1, in2, out, B, C, H, W, s2, kHalf ? 1 : 0,
+                                             layout, divisor, stream);
+    // a strip launcher declines a divisor other than its compile-time C (no C ABI entry passes
+    // one: Correlation divides by k^2 C); where no stream geometry takes such a grid either,
+    // the later stages below serve it
+    if (e != hipErrorNotSupported) return e;
+  }
   if (path == kPathBand)
     return warp_corr_band_f32(in1, in2, nullptr, nullptr, out, B, C, H, W, divisor, 0, stream);
   if (path == kPathRows)

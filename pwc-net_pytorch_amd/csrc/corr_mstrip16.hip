@@ -567,13 +567,10 @@ hipError_t launch(const void* in1, const void* in2, void* out, int B, int H, int
   const long long nblk = grid_blocks<G>(B, H, W);
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
+  {  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
     const hipError_t e =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_mstrip16<G>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+        lds_limit(reinterpret_cast<const void*>(&corr_fwd_mstrip16<G>), G::LDS_BYTES);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
 #ifdef PWC_CENSUS
   const int abl = debug_knob("ms_abl", 0);

@@ -398,13 +398,9 @@ static hipError_t launch_pt(const void* in1, const void* in2, void* out, int B, 
   const long long nblk = (long long)B * 2 * n_tr * n_tx;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_pt<G>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       G::LDS_BYTES);
+  {  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
+    const hipError_t e = lds_limit(reinterpret_cast<const void*>(&corr_fwd_pt<G>), G::LDS_BYTES);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   int ex;
   const float m = std::frexp(divisor, &ex);

@@ -485,13 +485,10 @@ hipError_t corr_forward_rows(const void* in1, const void* in2, void* out, int B,
   take_launch_events(&ev0, &ev1);
 #define PWC_ROWS(TT, RR, M1, M2)                                                              \
   if (sizeof(TT) == (h16 ? 2u : 4u) && R == RR && per1 <= M1 && per2 <= M2) {                 \
-    static bool attr = false;                                                                 \
-    if (!attr) {                                                                              \
-      hipError_t e = hipFuncSetAttribute(                                                     \
-          reinterpret_cast<const void*>(&corr_fwd_rows<TT, RR, NT, M1, M2>),                  \
-          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+    {  /* > 64 KiB dynamic LDS, once per device (capi.hip) */                                 \
+      const hipError_t e = lds_limit(                                                         \
+          reinterpret_cast<const void*>(&corr_fwd_rows<TT, RR, NT, M1, M2>), 160 * 1024);     \
       if (e != hipSuccess) return e;                                                          \
-      attr = true;                                                                            \
     }                                                                                         \
     hipExtLaunchKernelGGL((corr_fwd_rows<TT, RR, NT, M1, M2>), dim3((unsigned)g.units),       \
                           dim3(NT), lds, stream, ev0, ev1, 0, (const TT*)in1, (const TT*)in2, \
@@ -527,14 +524,12 @@ hipError_t corr_forward_rows_pair(const void* a1, const void* a2, void* aout, in
 #define PWC_ROWS_PAIR(RA, M1A, M2A, RB, M1B, M2B)                                             \
   if (pa.R == RA && pa.per1 <= M1A && pa.per2 <= M2A && pb.R == RB && pb.per1 <= M1B &&       \
       pb.per2 <= M2B) {                                                                       \
-    static bool attr = false;                                                                 \
-    if (!attr) {                                                                              \
-      hipError_t e = hipFuncSetAttribute(                                                     \
+    {  /* > 64 KiB dynamic LDS, once per device (capi.hip) */                                 \
+      const hipError_t e = lds_limit(                                                         \
           reinterpret_cast<const void*>(                                                      \
               &corr_fwd_rows_pair<float, RA, M1A, M2A, RB, M1B, M2B, NT>),                    \
-          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+          160 * 1024);                                                                      \
       if (e != hipSuccess) return e;                                                          \
-      attr = true;                                                                            \
     }                                                                                         \
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                  \
     take_launch_events(&ev0, &ev1); /* the one-shot timing hook times this launch */          \

@@ -321,12 +321,9 @@ static hipError_t launch_small(const void* in1, const void* in2, void* out, int 
   if (lds > 163840) return hipErrorNotSupported;
   if (nsplit > 1 && !partial) return hipErrorNotSupported;
   if (nsplit > 16) return hipErrorNotSupported;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_small<G>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  {  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
+    const hipError_t e = lds_limit(reinterpret_cast<const void*>(&corr_fwd_small<G>), 163840);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   int ex;
   const float m = std::frexp(divisor, &ex);

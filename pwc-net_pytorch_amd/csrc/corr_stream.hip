@@ -688,13 +688,10 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   if (nblk <= 0) return hipSuccess;
   if (C <= 0 || C % (G::NS * G::CC * G::CPU)) return hipErrorNotSupported;  // whole rounds
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&corr_fwd_stream<G>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  {  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
+    const hipError_t e =
+        lds_limit(reinterpret_cast<const void*>(&corr_fwd_stream<G>), G::LDS_BYTES);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   int ex;
   const float m = std::frexp(divisor, &ex);

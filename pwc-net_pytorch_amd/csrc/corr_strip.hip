@@ -197,6 +197,18 @@ constexpr int pair_group(int k) {
   return g < G::IPR - 1 ? g : G::IPR - 1;
 }
 
+// Step 0's barrier count must match the loader's: a compute wave takes one barrier at the step's
+// start (group 0) and one more each time pair_group rises, the loader one per DMA group.  That
+// holds iff pair_group starts at 0, rises by at most 1 per channel pair (NCS * QR + 2 <= 64:
+// a pair never spans two whole DMA groups) and ends at the last group.
+template <class G>
+constexpr bool pair_groups_match_loader() {
+  if (pair_group<G>(0) != 0 || pair_group<G>(G::CH - 1) != G::IPR - 1) return false;
+  for (int k = 1; k < G::CH; ++k)
+    if (pair_group<G>(k) - pair_group<G>(k - 1) > 1) return false;
+  return true;
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
@@ -380,6 +392,7 @@ template <class G>
 __global__ __launch_bounds__(G::THREADS, 1) void corr_fwd_strip(
     const float* __restrict__ in1, const float* __restrict__ in2, float* __restrict__ out,
     int H, int W, int ngrp, int ntx, OutEpi epi) {
+  static_assert(pair_groups_match_loader<G>(), "step-0 barriers out of step with the loader");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // logical block = (n, row parity, row group, strip, task group), task group fastest: the
   // workgroups of one image parity are neighbours and xcd_remap keeps neighbours on one XCD
@@ -585,13 +598,9 @@ static hipError_t launch(const void* in1, const void* in2, void* out, int B, int
   const long long nblk = (long long)B * 2 * ngrp * ntx * G::TS;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&corr_fwd_strip<G>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             G::LDS_ALLOC);
+  {  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
+    const hipError_t e = lds_limit(reinterpret_cast<const void*>(&corr_fwd_strip<G>), G::LDS_ALLOC);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   // the kernel divides by its compile-time C: Correlation's divisor k^2 C with k = 1
   if (divisor != (float)G::C) return hipErrorNotSupported;
@@ -639,7 +648,11 @@ using GeoF2 = Geo<PWC_STRIP_GEOF2>;
 // 56 (strips), C = 64 at W = 56 and C = 96 at W = 28 (whole rows).  Knobs: strip=0 disables the kernel
 // (measurement of the stream / row-band kernels), strip_geo=4 selects the 56-px strips at
 // W = 112, strip_l3=0 / strip_l2=0 leave C = 64 / 96 to the row-band kernel.
-enum StripPlan : int { kStripNone = 0, kStripL4 = 1, kStripF = 2, kStripF3 = 3, kStripF2 = 4 };
+enum StripPlan : int { kStripNone = 0, kStripL4 = 1, kStripF = 2, kStripF3 = 3, kStripF2 = 4,
+                       kStripD = 5 };
+long long dstrip_grid_blocks(int B, int H);  // corr_dstrip.hip
+hipError_t corr_forward_dstrip(const void* in1, const void* in2, void* out, int B, int H,
+                               float divisor, hipStream_t stream);
 static int strip_plan(const void* in1, const void* in2, const void* out, int B, int C, int H,
                       int W, int s2, int dtype, int layout) {
   if (dtype != 0 || s2 != 2 || layout != kRaster) return kStripNone;
@@ -651,7 +664,11 @@ static int strip_plan(const void* in1, const void* in2, const void* out, int B, 
   if (!(current_epi().slope <= 1.f)) return kStripNone;  // the max(v, slope v) epilogue
   if (debug_knob("strip", 1) == 0) return kStripNone;
   if (C == 32) {
-    if (W == strip::GeoF::TW && debug_knob("strip_geo", 5) != 4 &&
+    // W = 112: the displacement-diagonal strip (corr_dstrip.hip) unless strip_geo selects the
+    // whole-row (10) or 56-px (4) geometry of this file
+    const int geo = debug_knob("strip_geo", 20);
+    if (W == 112 && geo == 20 && dstrip_grid_blocks(B, H) >= 192) return kStripD;
+    if (W == strip::GeoF::TW && geo != 4 &&
         strip::grid_blocks<strip::GeoF>(B, H, W) >= 192)
       return kStripF;
     if (W % strip::GeoL4::TW == 0 && strip::grid_blocks<strip::GeoL4>(B, H, W) >= 192)
@@ -674,6 +691,8 @@ bool corr_strip_accepts(const void* in1, const void* in2, const void* out, int B
 hipError_t corr_forward_strip(const void* in1, const void* in2, void* out, int B, int C, int H,
                               int W, float divisor, hipStream_t stream) {
   switch (strip_plan(in1, in2, out, B, C, H, W, 2, 0, kRaster)) {
+    case kStripD:
+      return corr_forward_dstrip(in1, in2, out, B, H, divisor, stream);
     case kStripF:
       return strip::launch<strip::GeoF>(in1, in2, out, B, H, W, divisor, stream);
     case kStripF3:

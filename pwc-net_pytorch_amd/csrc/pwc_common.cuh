@@ -157,6 +157,11 @@ struct WarpProblem {
 // Kernels never read it -- launchers turn a knob into a template choice or an argument.
 int debug_knob(const char* name, int def);
 
+// Opt `kernel` in to `bytes` of dynamic LDS (more than 64 KiB needs hipFuncSetAttribute) on the
+// CURRENT device.  The attribute is per device, so the launchers' one-time opt-in is cached per
+// (kernel, device): a process that launches on several devices sets it on each (capi.hip).
+hipError_t lds_limit(const void* kernel, int bytes);
+
 // XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle must
 // be bijective"): consecutive logical tiles land on the same XCD (and L2), so neighbouring
 // tiles that re-read each other's halo rows hit the same L2.  Pure speed choice.

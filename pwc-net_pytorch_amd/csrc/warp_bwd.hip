@@ -578,14 +578,11 @@ hipError_t warp_backward_tiles_f32(const void* x, const void* flow, const void* 
   a.census = debug_knob("warp_bwd_census", 0);
   const unsigned grid = (unsigned)(B * p.ntiles * p.ng);
   constexpr size_t lds = (size_t)2 * WN * 4 * sizeof(float) + (size_t)MAXE * sizeof(int2);
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(&warp_bwd_tile<4, true>),
-                          reinterpret_cast<const void*>(&warp_bwd_tile<4, false>)}) {
-      e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-    }
-    attr = true;
+  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
+  for (const void* f : {reinterpret_cast<const void*>(&warp_bwd_tile<4, true>),
+                        reinterpret_cast<const void*>(&warp_bwd_tile<4, false>)}) {
+    e = lds_limit(f, (int)lds);
+    if (e != hipSuccess) return e;
   }
   if (W % 4 == 0)
     hipLaunchKernelGGL((warp_bwd_tile<4, true>), dim3(grid), dim3(NT), lds, stream, a);

@@ -443,13 +443,10 @@ static bool env_cfg(int* R, int* T, int* G) {
 
 template <typename E, int R, int T, bool WARP>
 static hipError_t launch(const Prob& P, size_t lds, hipStream_t stream) {
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&warp_corr_band<E, R, T, WARP>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  {  // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
+    const hipError_t e =
+        lds_limit(reinterpret_cast<const void*>(&warp_corr_band<E, R, T, WARP>), 160 * 1024);
     if (e != hipSuccess) return e;
-    attr = true;
   }
   const int ntg = (D + T - 1) / T;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -637,13 +634,10 @@ hipError_t warp_corr_band_pair(const BandProblem& a, const BandProblem& b, float
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 #define PWC_PAIR_E(E, A0, B0, A1, B1)                                                         \
   {                                                                                           \
-    static bool attr = false;                                                                 \
-    if (!attr) {                                                                              \
-      hipError_t e = hipFuncSetAttribute(                                                     \
-          reinterpret_cast<const void*>(&warp_corr_band_pair<E, A0, B0, A1, B1>),             \
-          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                            \
+    {  /* > 64 KiB dynamic LDS, once per device (capi.hip) */                                 \
+      const hipError_t e = lds_limit(                                                         \
+          reinterpret_cast<const void*>(&warp_corr_band_pair<E, A0, B0, A1, B1>), 160 * 1024);\
       if (e != hipSuccess) return e;                                                          \
-      attr = true;                                                                            \
     }                                                                                         \
     take_launch_events(&ev0, &ev1);                                                           \
     hipExtLaunchKernelGGL((warp_corr_band_pair<E, A0, B0, A1, B1>),                           \

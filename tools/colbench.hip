@@ -24,6 +24,9 @@ void take_launch_events(hipEvent_t* a, hipEvent_t* b) {
   g_e0 = g_e1 = nullptr;
 }
 OutEpi current_epi() { return OutEpi{0, 1.f}; }
+hipError_t lds_limit(const void* k, int bytes) {  // one device here
+  return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
 int debug_knob(const char*, int def) { return def; }
 }  // namespace pwc
 
