@@ -648,11 +648,7 @@ using GeoF2 = Geo<PWC_STRIP_GEOF2>;
 // 56 (strips), C = 64 at W = 56 and C = 96 at W = 28 (whole rows).  Knobs: strip=0 disables the kernel
 // (measurement of the stream / row-band kernels), strip_geo=4 selects the 56-px strips at
 // W = 112, strip_l3=0 / strip_l2=0 leave C = 64 / 96 to the row-band kernel.
-enum StripPlan : int { kStripNone = 0, kStripL4 = 1, kStripF = 2, kStripF3 = 3, kStripF2 = 4,
-                       kStripD = 5 };
-long long dstrip_grid_blocks(int B, int H);  // corr_dstrip.hip
-hipError_t corr_forward_dstrip(const void* in1, const void* in2, void* out, int B, int H,
-                               float divisor, hipStream_t stream);
+enum StripPlan : int { kStripNone = 0, kStripL4 = 1, kStripF = 2, kStripF3 = 3, kStripF2 = 4 };
 static int strip_plan(const void* in1, const void* in2, const void* out, int B, int C, int H,
                       int W, int s2, int dtype, int layout) {
   if (dtype != 0 || s2 != 2 || layout != kRaster) return kStripNone;
@@ -664,11 +660,7 @@ static int strip_plan(const void* in1, const void* in2, const void* out, int B, 
   if (!(current_epi().slope <= 1.f)) return kStripNone;  // the max(v, slope v) epilogue
   if (debug_knob("strip", 1) == 0) return kStripNone;
   if (C == 32) {
-    // W = 112: the displacement-diagonal strip (corr_dstrip.hip) unless strip_geo selects the
-    // whole-row (10) or 56-px (4) geometry of this file
-    const int geo = debug_knob("strip_geo", 20);
-    if (W == 112 && geo == 20 && dstrip_grid_blocks(B, H) >= 192) return kStripD;
-    if (W == strip::GeoF::TW && geo != 4 &&
+    if (W == strip::GeoF::TW && debug_knob("strip_geo", 10) != 4 &&
         strip::grid_blocks<strip::GeoF>(B, H, W) >= 192)
       return kStripF;
     if (W % strip::GeoL4::TW == 0 && strip::grid_blocks<strip::GeoL4>(B, H, W) >= 192)
@@ -691,8 +683,6 @@ bool corr_strip_accepts(const void* in1, const void* in2, const void* out, int B
 hipError_t corr_forward_strip(const void* in1, const void* in2, void* out, int B, int C, int H,
                               int W, float divisor, hipStream_t stream) {
   switch (strip_plan(in1, in2, out, B, C, H, W, 2, 0, kRaster)) {
-    case kStripD:
-      return corr_forward_dstrip(in1, in2, out, B, H, divisor, stream);
     case kStripF:
       return strip::launch<strip::GeoF>(in1, in2, out, B, H, W, divisor, stream);
     case kStripF3:

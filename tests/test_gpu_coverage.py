@@ -135,30 +135,6 @@ def test_strip_56px_geometry_at_w112(shape):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("shape", [(8, 32, 96, 112), (6, 32, 95, 112), (8, 32, 90, 112)],
-                         ids=["l4", "b6_odd", "partial_band"])
-def test_dstrip_equals_full_row_strip(shape):
-    """The l4 displacement-diagonal strip (corr_dstrip.hip, the default at W = 112) against the
-    oracle, and bit for bit against the whole-row strip geometry GeoF (knob strip_geo=10): both
-    sum each channel half in channel order and then the halves.  Odd heights and a partial last
-    band (45 parity rows in bands of 3) included."""
-    from pwcnet_amd import _lib
-    from pwcnet_amd.ops import corr_forward
-    B, C, H, W = shape
-    assert _lib.corr_forward_plan(B, C, H, W, 9, 1, 9, 1, 2) == "strip"
-    a, an = _rand(shape, torch.float32, "dsa", shape)
-    b, bn = _rand(shape, torch.float32, "dsb", shape)
-    out = corr_forward(a, b, 9, 1, 9, 1, 2)
-    _lib.set_debug("strip_geo=10")
-    try:
-        ref = corr_forward(a, b, 9, 1, 9, 1, 2)
-        torch.cuda.synchronize()
-    finally:
-        _lib.set_debug("")
-    _check(out, O.corr_forward(an, bn, 9, 1, 9, 1, 2), torch.float32)
-    assert torch.equal(out, ref)
-
-
 @pytest.mark.parametrize("shape", [(8, 32, 96, 112), (8, 64, 48, 56), (8, 96, 24, 28)],
                          ids=["l4", "l3", "l2"])
 def test_corr_md8_forward_strip_vs_oracle(shape):
@@ -208,18 +184,15 @@ def test_cost_volume_448x1024_b4(shape):
     _check(out, O.cvl_forward(an, bn, 4), torch.float32)
 
 
-@pytest.mark.parametrize("shape,knob,geo", [((8, 96, 24, 28), "strip_l2=0", ""),
-                                            ((8, 64, 48, 56), "strip_l3=0", ""),
-                                            ((8, 32, 96, 112), "strip_geo=4", "strip_geo=10"),
-                                            ((8, 32, 96, 112), "strip_geo=10", "")],
-                         ids=["l2", "l3", "l4_geof", "l4_dstrip"])
-def test_strip_full_rows_after_other_kernels(shape, knob, geo):
+@pytest.mark.parametrize("shape,knob", [((8, 96, 24, 28), "strip_l2=0"),
+                                        ((8, 64, 48, 56), "strip_l3=0"),
+                                        ((8, 32, 96, 112), "strip_geo=4")], ids=["l2", "l3", "l4"])
+def test_strip_full_rows_after_other_kernels(shape, knob):
     """The whole-row strip geometries read each channel row's right halo from the next channel
     row's zero pad: a read issued before that pad's DMA group landed returns whatever LDS held
     (a round-5 bug at C = 64, caught only with other kernels' data left in LDS).  Each round
-    runs the reference-path kernel (knob) on unrelated data first, then the kernel under test
-    (`geo`: the default, or GeoF at l4) on fresh inputs, against the oracle; at l4 also the
-    displacement-diagonal strip (the default) after GeoF's junk run."""
+    runs the reference-path kernel (knob) on unrelated data first, then the default on fresh
+    inputs, against the oracle."""
     from pwcnet_amd import _lib
     from pwcnet_amd.ops import corr_forward
     for it in range(4):
@@ -231,24 +204,19 @@ def test_strip_full_rows_after_other_kernels(shape, knob, geo):
             _lib.set_debug("")
         a, an = _rand(shape, torch.float32, "sa", it, shape)
         b, bn = _rand(shape, torch.float32, "sb", it, shape)
-        _lib.set_debug(geo)
-        try:
-            out = corr_forward(a, b, 9, 1, 9, 1, 2)
-            torch.cuda.synchronize()
-        finally:
-            _lib.set_debug("")
+        out = corr_forward(a, b, 9, 1, 9, 1, 2)
+        torch.cuda.synchronize()
         _check(out, O.corr_forward(an, bn, 9, 1, 9, 1, 2), torch.float32)
 
 
 @pytest.mark.parametrize("shape,knob", [((8, 64, 48, 56), "strip_l3=0"),
                                         ((8, 96, 24, 28), "strip_l2=0"),
-                                        ((8, 32, 96, 112), "strip_geo=10")],
+                                        ((8, 32, 96, 112), "strip_geo=4")],
                          ids=["l3", "l2", "l4"])
 def test_strip_c64_into_cat_slice_leaky(shape, knob):
     """model.py:83-84 + :89/91 at config 2's l3 / l2 / l4 (C = 64 / 96 / 32, B = 8) through the
-    strip kernels (whole-row geometries; the displacement-diagonal strip at l4): the cat slice
-    with leaky_relu(0.01) fused; the other kernel's volume (knob: row band, GeoF at l4) against
-    the oracle too."""
+    strip kernel's whole-row geometries: the cat slice with leaky_relu(0.01) fused; the other
+    kernel's volume (knob: row band; the 56-px strips at l4) against the oracle too."""
     from pwcnet_amd import _lib
     from pwcnet_amd.ops import corr_forward, corr_forward_into
     B, C, H, W = shape

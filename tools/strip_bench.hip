@@ -19,7 +19,6 @@
 #include "../pwc-net_pytorch_amd/csrc/corr_stream.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_strip.hip"
 #include "../pwc-net_pytorch_amd/csrc/corr_mstrip16.hip"
-#include "../pwc-net_pytorch_amd/csrc/corr_dstrip.hip"
 
 namespace pwc {
 hipEvent_t g_e0 = nullptr, g_e1 = nullptr;
@@ -81,7 +80,6 @@ static auto with_geo(F&& f) {
   }
 }
 static hipError_t strip_call(const void* a, const void* b, void* o, int B, int H, int W) {
-  if (g_geo == 20) return pwc::corr_forward_dstrip(a, b, o, B, H, 32.f, 0);  // corr_dstrip.hip
   return with_geo([&](auto g) {
     return pwc::strip::launch<decltype(g)>(a, b, o, B, H, W, 32.f, 0);
   });
@@ -120,7 +118,7 @@ int main(int argc, char** argv) {
   const int H = argc > 3 ? std::atoi(argv[3]) : 96;
   const int W = argc > 4 ? std::atoi(argv[4]) : 112;
   const int C = 32;
-  g_geo = pwc::debug_knob("strip_geo", 20);
+  g_geo = pwc::debug_knob("strip_geo", 10);
   {
     unsigned* d;
     CK(hipMalloc(&d, 128 * 4));
@@ -301,61 +299,11 @@ int main(int argc, char** argv) {
     vb.push_back(ms * 1e3);
   }
   std::sort(vb.begin(), vb.end());
-#ifdef PWC_DSTRIP_CENSUS
-  {
-    // the diagonal strip's census: per stamp, the mean over workgroups of (stamp - own entry)
-    // and the latest workgroup relative to the launch's earliest entry (us)
-    const int nb = (int)pwc::dstrip_grid_blocks(B, H), CI = 50;
-    unsigned long long* cen;
-    CK(hipMalloc(&cen, (size_t)CI * nb * 64 * 8));
-    CK(hipMemset(cen, 0, (size_t)CI * nb * 64 * 8));
-    for (int i = 0; i < CI; ++i) {
-      unsigned long long* p = cen + (size_t)i * nb * 64;
-      CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::dstrip::g_dcensus), &p, sizeof(p)));
-      CK(strip_call(f1[i % NS], f2[i % NS], o2[i % NS], B, H, W));
-    }
-    unsigned long long* np = nullptr;
-    CK(hipMemcpyToSymbol(HIP_SYMBOL(pwc::dstrip::g_dcensus), &np, sizeof(np)));
-    CK(hipDeviceSynchronize());
-    std::vector<unsigned long long> c((size_t)CI * nb * 64);
-    CK(hipMemcpy(c.data(), cen, c.size() * 8, hipMemcpyDeviceToHost));
-    double mx[64] = {}, mean[64] = {}, skew = 0;
-    for (int i = 0; i < CI; ++i) {
-      const unsigned long long* L = c.data() + (size_t)i * nb * 64;
-      unsigned long long t0 = ~0ull, t0max = 0;
-      for (int b = 0; b < nb; ++b) {
-        t0 = std::min(t0, L[b * 64]);
-        t0max = std::max(t0max, L[b * 64]);
-      }
-      skew += (t0max - t0) * 0.01;
-      for (int k = 1; k < 64; ++k) {
-        unsigned long long m = 0;
-        double sm = 0;
-        for (int b = 0; b < nb; ++b) {
-          m = std::max(m, L[b * 64 + k]);
-          sm += L[b * 64 + k] ? (double)(L[b * 64 + k] - L[b * 64]) : 0.0;
-        }
-        mx[k] += m ? (m - t0) * 0.01 : 0.0;
-        mean[k] += sm / nb * 0.01;
-      }
-    }
-    std::printf("{\"census\": \"dstrip\", \"start_skew_us\": %.2f", skew / CI);
-    std::printf(", \"B_m\": [");
-    for (int k = 1; k <= 11; ++k) std::printf("%s%.2f", k > 1 ? ", " : "", mean[k] / CI);
-    std::printf("], \"stored_m\": [");
-    for (int k = 12; k <= 22; ++k) std::printf("%s%.2f", k > 12 ? ", " : "", mean[k] / CI);
-    std::printf("], \"row_landed\": [");
-    for (int k = 32; k <= 42; ++k) std::printf("%s%.2f", k > 32 ? ", " : "", mean[k] / CI);
-    std::printf("], \"loader_entry\": %.2f, \"latest_stored_10\": %.2f}  (mean per-workgroup us after entry)\n",
-                mean[43] / CI, mx[22] / CI);
-  }
-#endif
 #ifdef PWC_STRIP_CENSUS
   {
     // one more batch of launches with the census buffer armed: per launch, each stamp's
     // LATEST workgroup relative to the launch's earliest workgroup start, and the mean
     // per-workgroup span from its own start (us); quad A = wave 0, quad B = wave WPP
-    if (g_geo == 20) return 0;  // no census in the diagonal kernel
     const int nb = (int)with_geo([&](auto g) {
       return pwc::strip::grid_blocks<decltype(g)>(B, H, W);
     });
