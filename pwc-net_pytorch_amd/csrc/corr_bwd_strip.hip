@@ -418,8 +418,9 @@ using GeoB2 = Geo<PWC_BWD_GEO2>;
 
 // Which geometry serves this problem (0: none): fp32 (the caller checks model.py:24's
 // configuration: k 1, s1 1, s2 2, pad == md in {8, 9}, raster), 16-B aligned buffers, the
-// widths and channel counts of the geometries, 32-bit buffer offsets.  Knob bwd_strip=0
-// leaves every problem to corr_bwd_rows.hip.
+// widths and channel counts of the geometries, 32-bit buffer offsets, a grid of >= 192
+// workgroups.  Knob bwd_strip=0 leaves every problem to corr_bwd_rows.hip, bwd_strip=2 drops
+// the grid-size condition.
 static int bwd_strip_plan(const void* in1, const void* in2, const void* gout, const void* g1,
                           const void* g2, int B, int C, int H, int W) {
   if (debug_knob("bwd_strip", 1) == 0 || B <= 0 || H < 2) return 0;
@@ -427,11 +428,22 @@ static int bwd_strip_plan(const void* in1, const void* in2, const void* gout, co
       (uintptr_t)g1 % 16 || (uintptr_t)g2 % 16)
     return 0;
   if ((size_t)81 * H * W * 4 >= 0x7ffffff0ull || (size_t)C * H * W * 4 >= 0x7ffffff0ull) return 0;
-  // every geometry stages all C channels in one workgroup (CW = C: the kernel divides by CW)
-  if (C == 32 && W == 4 * bstrip::GeoB4::NSEG && C == bstrip::GeoB4::CW) return 4;
-  if (C == 64 && W == 4 * bstrip::GeoB3::NSEG && C == bstrip::GeoB3::CW) return 3;
+  // every geometry stages all C channels in one workgroup (CW = C: the kernel divides by CW);
+  // and the grid must fill the chip: its latency-bound workgroups (9 dependent steps each) lose
+  // to corr_bwd_rows.hip below ~192 of them (profiles/r06c_bwd_strip_small_batch.txt: B = 1 / 2
+  // at l2-l4, B = 4 at l2 / l3 -- 8.4-13.2 against 10.4-15.9 us; B = 4 at l4, 256 workgroups,
+  // 17.7 against 18.4)
+  // (knob bwd_strip = 2: any grid -- the small-batch edge-case tests of the kernel)
+  const bool any_grid = debug_knob("bwd_strip", 1) == 2;
+  auto fills = [&](int R) {
+    return any_grid || 2LL * B * 2 * (((H + 1) / 2 + R - 1) / R) >= 192;
+  };
+  if (C == 32 && W == 4 * bstrip::GeoB4::NSEG && C == bstrip::GeoB4::CW && fills(bstrip::GeoB4::R))
+    return 4;
+  if (C == 64 && W == 4 * bstrip::GeoB3::NSEG && C == bstrip::GeoB3::CW && fills(bstrip::GeoB3::R))
+    return 3;
   if (C == 96 && W == 4 * bstrip::GeoB2::NSEG && C == bstrip::GeoB2::CW &&
-      debug_knob("bwd_strip_l2", 1) != 0)
+      fills(bstrip::GeoB2::R) && debug_knob("bwd_strip_l2", 1) != 0)
     return 2;
   return 0;
 }

@@ -33,6 +33,11 @@ constexpr int WS = TS + 2 * MG;   // window side (32)
 constexpr int WN = WS * WS;       // window pixels (1024)
 constexpr int MAXE = 4 * WN;      // list entries (each window pixel has 4 corners)
 constexpr size_t kHead = 256;     // workspace: header, then partials / far lists / far counts
+#ifndef PWC_WBWD_CC  // channels per chunk (measurement builds may override)
+#define PWC_WBWD_CC 4
+#endif
+constexpr int CC = PWC_WBWD_CC;
+constexpr int MINWG = CC <= 4 ? 2 : 1;  // workgroups per CU the LDS allows
 
 struct Args {
   const float* x;
@@ -101,7 +106,7 @@ __device__ __forceinline__ float corner_w(const Bilinear& b, int k) {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int CC, bool V4>
-__global__ __launch_bounds__(NT, 2) void warp_bwd_tile(Args a) {
+__global__ __launch_bounds__(NT, MINWG) void warp_bwd_tile(Args a) {
   constexpr int NW = NT / 64;     // waves
   constexpr int HC = CC / 2;      // channels of a chunk per half (threads t, t + 256)
   __shared__ int cnt[NW][256];
@@ -499,7 +504,7 @@ static bool plan(int B, int C, int H, int W, Plan* p) {
   p->ntiles = p->ntx * ((H + TS - 1) / TS);
   const long long tiles = (long long)B * p->ntiles;
   // channel groups: at most 512 workgroups (two per CU: one round), at least 4 channels each
-  const int cc = 4;
+  const int cc = CC;
   long long ng = 512 / tiles;
   const long long maxg = (C + cc - 1) / cc;
   if (ng > maxg) ng = maxg;
@@ -577,17 +582,17 @@ hipError_t warp_backward_tiles_f32(const void* x, const void* flow, const void* 
   a.nwg = p.nwg;
   a.census = debug_knob("warp_bwd_census", 0);
   const unsigned grid = (unsigned)(B * p.ntiles * p.ng);
-  constexpr size_t lds = (size_t)2 * WN * 4 * sizeof(float) + (size_t)MAXE * sizeof(int2);
+  constexpr size_t lds = (size_t)2 * WN * CC * sizeof(float) + (size_t)MAXE * sizeof(int2);
   // > 64 KiB dynamic LDS: opted in once per device (lds_limit, capi.hip)
-  for (const void* f : {reinterpret_cast<const void*>(&warp_bwd_tile<4, true>),
-                        reinterpret_cast<const void*>(&warp_bwd_tile<4, false>)}) {
+  for (const void* f : {reinterpret_cast<const void*>(&warp_bwd_tile<CC, true>),
+                        reinterpret_cast<const void*>(&warp_bwd_tile<CC, false>)}) {
     e = lds_limit(f, (int)lds);
     if (e != hipSuccess) return e;
   }
   if (W % 4 == 0)
-    hipLaunchKernelGGL((warp_bwd_tile<4, true>), dim3(grid), dim3(NT), lds, stream, a);
+    hipLaunchKernelGGL((warp_bwd_tile<CC, true>), dim3(grid), dim3(NT), lds, stream, a);
   else
-    hipLaunchKernelGGL((warp_bwd_tile<4, false>), dim3(grid), dim3(NT), lds, stream, a);
+    hipLaunchKernelGGL((warp_bwd_tile<CC, false>), dim3(grid), dim3(NT), lds, stream, a);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   unsigned fin = (unsigned)(((size_t)B * H * W + 255) / 256);

@@ -257,7 +257,11 @@ def test_corr_backward_plan_routes_and_declines():
     c9 = (9, 1, 9, 1, 2)
     assert plan(8, 32, 96, 112, *c9) == "strip"   # config 5 l4
     assert plan(8, 64, 48, 56, *c9) == "strip"    # config 5 l3
-    assert plan(1, 32, 7, 112, *c9) == "strip"    # a band taller than the image
+    assert plan(1, 32, 7, 112, *c9) == "rows"     # 8 workgroups: the row-band kernel
+    assert plan(4, 32, 96, 112, *c9) == "strip"   # 256 workgroups
+    assert plan(2, 32, 96, 112, *c9) == "rows"    # 128: below 192
+    assert plan(4, 64, 48, 56, *c9) == "rows"     # 128 at l3
+    assert plan(4, 96, 24, 28, *c9) == "rows"     # 96 at l2
     assert plan(8, 96, 24, 28, *c9) == "strip"    # l2
     assert plan(8, 96, 24, 30, *c9) == "rows"     # l2-like, another width
     assert plan(8, 192, 6, 7, *c9) == "rows"      # l0
