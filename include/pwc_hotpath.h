@@ -31,6 +31,9 @@
  *                             torch-0.4 semantics (bilinear, zeros, align_corners=True).
  *   pwc_warp_corr_forward  <- the two calls of one pyramid level, model.py:80 (warp) + :83
  *                             (corr), as one entry point (fused kernel where it applies).
+ *   pwc_warp_corr_backward <- their backward: Correlation_backward_cuda (correlation_cuda.c:
+ *                             95-180) into x2_warp, then grid_sample's backward (modules.py:41),
+ *                             as one entry point (one kernel at the coarse levels).
  *   pwc_upsample_warp_forward <- model.py:78 (F.upsample(flow, scale_factor=2,
  *                             mode='bilinear') * 2, torch-0.4 align_corners=False) + :80
  *                             (WarpingLayer) as one launch; pwc_flow_upsample_backward is the
@@ -253,6 +256,28 @@ PWC_API int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, i
                                         int pad_size, int kernel_size, int max_displacement,
                                         int stride1, int stride2, int corr_multiply, int dtype,
                                         void* stream);
+
+/* The backward of pwc_warp_corr_forward (WarpCorrelationFunction.backward): from grad_corr
+ * ([B][OC][Ho][Wo]) and an optional gradient arriving on x2_warp itself (grad_x2_warp, NULL =
+ * none) -> grad_in1 (d/dx1, as pwc_corr_backward's grad_in1), grad_x2 and grad_flow (the warp
+ * backward, as pwc_warp_backward_ws, of d/dx2_warp + grad_x2_warp).  fp32, stride1 == 1.
+ * `workspace`: at least pwc_warp_corr_backward_workspace_size() bytes.  `counters`: B uint32
+ * in device memory, zero before the first call; every call leaves them zero (one set per
+ * stream: concurrent calls must not share it); NULL selects the two-launch path.  For
+ * model.py:24's configuration on images of <= 256 pixels with C % 4 == 0 (the l0 / l1 levels)
+ * this is ONE kernel whose d/dx2_warp never leaves LDS; grad_flow then adds per-channel-group
+ * partials in a fixed order (deterministic).  Elsewhere: pwc_corr_backward into the workspace,
+ * the x2_warp gradient added, then pwc_warp_backward_ws. */
+PWC_API size_t pwc_warp_corr_backward_workspace_size(int B, int C, int H, int W, int pad_size,
+                                                     int kernel_size, int max_displacement,
+                                                     int stride1, int stride2, int dtype);
+PWC_API int pwc_warp_corr_backward(const void* in1, const void* x2, const void* flow,
+                                   const void* x2_warp, const void* grad_corr,
+                                   const void* grad_x2_warp, void* grad_in1, void* grad_x2,
+                                   void* grad_flow, int B, int C, int H, int W, int pad_size,
+                                   int kernel_size, int max_displacement, int stride1,
+                                   int stride2, int corr_multiply, int dtype, void* workspace,
+                                   size_t workspace_bytes, void* counters, void* stream);
 /* Several INDEPENDENT correlations (e.g. the bench's synthetic pyramid levels, or the levels
  * of different batches in flight; inside one model forward each level's correlation needs that
  * level's warp, which needs the previous level's flow).  Each problem's output equals a

@@ -167,11 +167,18 @@ bool corr_mstrip16_accepts(const void*, const void*, const void*, int, int, int,
                            int);
 bool corr_bwd_strip_accepts(const void*, const void*, const void*, const void*, const void*, int,
                             int, int, int);
+size_t warp_corr_bwd_small_workspace(int B, int C, int H, int W);
+hipError_t warp_corr_bwd_small(const void* in1, const void* x2, const void* flow,
+                               const void* x2w, const void* grad_corr, const void* grad_x2w,
+                               void* grad_in1, void* grad_x2, void* grad_flow, int B, int C,
+                               int H, int W, float divisor, void* ws, size_t ws_bytes,
+                               void* counters, hipStream_t stream);
+hipError_t add_inplace_f32(void* y, const void* x, size_t n, hipStream_t stream);
 }  // namespace pwc
 
 extern "C" {
 
-int pwc_abi_version(void) { return 10; }
+int pwc_abi_version(void) { return 11; }
 
 int pwc_corr_forward_plan(const void* in1, const void* in2, const void* out, int B, int C, int H,
                           int W, int pad_size, int kernel_size, int max_displacement, int stride1,
@@ -777,6 +784,72 @@ int pwc_warp_corr_forward_group(const pwc_warp_corr_problem* problems, int count
       return 0;
   }
   return 1;
+}
+
+// ---- the backward of one level (model.py:80-83) as one call ----
+// model.py:24's configuration in fp32 on images one workgroup holds (l0 / l1): one launch
+// (warp_corr_bwd.hip); otherwise the correlation backward into the workspace (d/dx2_warp), the
+// incoming x2_warp gradient added, and the warp backward (its workspace after that buffer).
+size_t pwc_warp_corr_backward_workspace_size(int B, int C, int H, int W, int pad_size,
+                                             int kernel_size, int max_displacement, int stride1,
+                                             int stride2, int dtype) {
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W) || dtype != PWC_DTYPE_F32 ||
+      !corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo) ||
+      Ho <= 0 || Wo <= 0)
+    return 0;
+  const size_t gw = ((size_t)B * C * H * W * sizeof(float) + 255) & ~(size_t)255;
+  const size_t two = gw + pwc::warp_backward_workspace_size(B, C, H, W);
+  size_t one = 0;
+  if (warp_corr_fusable(pad_size, kernel_size, max_displacement, stride1, stride2, dtype))
+    one = pwc::warp_corr_bwd_small_workspace(B, C, H, W);
+  return one > two ? one : two;
+}
+
+int pwc_warp_corr_backward(const void* in1, const void* x2, const void* flow,
+                           const void* x2_warp, const void* grad_corr, const void* grad_x2_warp,
+                           void* grad_in1, void* grad_x2, void* grad_flow, int B, int C, int H,
+                           int W, int pad_size, int kernel_size, int max_displacement,
+                           int stride1, int stride2, int corr_multiply, int dtype,
+                           void* workspace, size_t workspace_bytes, void* counters,
+                           void* stream) {
+  const char* fn = "pwc_warp_corr_backward";
+  int OC, Ho, Wo;
+  if (!dims_ok(B, C, H, W)) return fail(fn, "negative dimension");
+  if (dtype != PWC_DTYPE_F32) return fail(fn, "backward is fp32 only");
+  if (stride1 != 1) return fail(fn, "stride1 must be 1 (the reference backward is undefined)");
+  if (!corr_shape(H, W, pad_size, kernel_size, max_displacement, stride1, stride2, &OC, &Ho,
+                  &Wo))
+    return fail(fn, "invalid correlation parameters");
+  if (Ho <= 0 || Wo <= 0) return fail(fn, "empty correlation output");
+  if ((size_t)B * H * W == 0) return 1;
+  if (!in1 || !x2 || !flow || !x2_warp || !grad_corr || !grad_in1 || !grad_x2 || !grad_flow)
+    return fail(fn, "null buffer");
+  const size_t need = pwc_warp_corr_backward_workspace_size(
+      B, C, H, W, pad_size, kernel_size, max_displacement, stride1, stride2, dtype);
+  if (!workspace || workspace_bytes < need)
+    return fail(fn, "workspace smaller than pwc_warp_corr_backward_workspace_size()");
+  hipStream_t s = (hipStream_t)stream;
+  if (!fused_disabled() &&
+      warp_corr_fusable(pad_size, kernel_size, max_displacement, stride1, stride2, dtype)) {
+    const hipError_t e = pwc::warp_corr_bwd_small(
+        in1, x2, flow, x2_warp, grad_corr, grad_x2_warp, grad_in1, grad_x2, grad_flow, B, C, H,
+        W, (float)(kernel_size * kernel_size * C), workspace, workspace_bytes, counters, s);
+    if (e != hipErrorNotSupported) return check_launch(fn, e);
+  }
+  // two launches (+ the x2_warp gradient): gw in the workspace head
+  void* gw = workspace;
+  const size_t gwb = ((size_t)B * C * H * W * sizeof(float) + 255) & ~(size_t)255;
+  if (!pwc_corr_backward(in1, x2_warp, grad_corr, grad_in1, gw, B, C, H, W, pad_size,
+                         kernel_size, max_displacement, stride1, stride2, corr_multiply, dtype,
+                         stream))
+    return 0;
+  if (grad_x2_warp &&
+      !check_launch(fn, pwc::add_inplace_f32(gw, grad_x2_warp, (size_t)B * C * H * W, s)))
+    return 0;
+  return pwc_warp_backward_ws(x2, flow, gw, grad_x2, grad_flow, B, C, H, W, dtype,
+                              (char*)workspace + gwb, workspace_bytes - gwb, stream);
 }
 
 }  // extern "C"

@@ -71,6 +71,8 @@ SYMBOLS = {
     "pwc_warp_corr_workspace_size": (_Z, [_I] * 11),
     "pwc_warp_corr_forward": (_I, [_P] * 5 + [_I] * 11 + [_P, _Z, _P]),
     "pwc_warp_corr_forward_group": (_I, [ctypes.POINTER(WarpCorrProblem)] + [_I] * 8 + [_P]),
+    "pwc_warp_corr_backward_workspace_size": (_Z, [_I] * 10),
+    "pwc_warp_corr_backward": (_I, [_P] * 9 + [_I] * 11 + [_P, _Z, _P, _P]),
     "pwc_corr_forward_group": (_I, [ctypes.POINTER(CorrProblem)] + [_I] * 8 + [_P]),
     "pwc_warp_forward_group": (_I, [ctypes.POINTER(WarpProblem), _I, _I, _P]),
     "pwc_upsample_warp_forward": (_I, [_P] * 4 + [_I] * 5 + [_P]),
@@ -79,7 +81,7 @@ SYMBOLS = {
     "pwc_corr_forward_into": (_I, [_P, _P, _P, ctypes.c_longlong, ctypes.c_float] + [_I] * 11
                               + [_P, _Z, _P]),
 }
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lock = threading.Lock()
 _lib = None

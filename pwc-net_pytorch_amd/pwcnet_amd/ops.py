@@ -520,10 +520,76 @@ def warp_corr_forward_group(problems, pad_size, kernel_size, max_displacement, s
     return outs
 
 
+# Arrival counters of the one-launch level backward (pwc_warp_corr_backward): B uint32 per
+# device, zeroed once here (outside any graph capture, so captured replays reuse them); every
+# call leaves them zero.  One set per device: level backwards of one device must not run
+# concurrently on two streams (autograd runs a device's backward on one stream).
+_COUNTERS = {}
+
+
+def _counters(B, device):
+    c = _COUNTERS.get(device)
+    if c is None or c.numel() < B:
+        if torch.cuda.is_current_stream_capturing():
+            return None  # not allocated inside a capture: the two-launch path runs instead
+        c = torch.zeros(max(B, 64), dtype=torch.int32, device=device)
+        _COUNTERS[device] = c
+    return c
+
+
+def warp_corr_backward(input1, x2, flow, x2_warp, grad_corr, pad_size, kernel_size,
+                       max_displacement, stride1, stride2, corr_multiply=1, grad_x2_warp=None):
+    """(grad_input1, grad_x2, grad_flow): the backward of ``warp_corr_forward`` --
+    ``corr_backward(input1, x2_warp, grad_corr)`` then ``warp_backward(x2, flow, d/dx2_warp +
+    grad_x2_warp)`` -- as one C call (pwc_warp_corr_backward; one kernel at the coarse levels of
+    model.py:24's configuration, where d/dx2_warp never leaves LDS)."""
+    _check_inputs("WarpCorrelation backward", input1, x2, flow, x2_warp, grad_corr,
+                  dtypes=(torch.float32,))
+    B, C, H, W = input1.shape
+    if tuple(x2.shape) != (B, C, H, W) or tuple(x2_warp.shape) != (B, C, H, W):
+        raise ValueError("WarpCorrelation backward: input shapes differ")
+    if tuple(flow.shape) != (B, 2, H, W):
+        raise ValueError(f"WarpCorrelation backward: flow shape {tuple(flow.shape)} != "
+                         f"{(B, 2, H, W)}")
+    OC, Ho, Wo = _lib.corr_output_shape(H, W, pad_size, kernel_size, max_displacement, stride1,
+                                        stride2)
+    if tuple(grad_corr.shape) != (B, OC, Ho, Wo):
+        raise ValueError(f"WarpCorrelation backward: grad shape {tuple(grad_corr.shape)} != "
+                         f"{(B, OC, Ho, Wo)}")
+    if grad_x2_warp is not None:
+        _check_inputs("WarpCorrelation backward", grad_x2_warp, dtypes=(torch.float32,))
+        if tuple(grad_x2_warp.shape) != (B, C, H, W):
+            raise ValueError("WarpCorrelation backward: grad_x2_warp shape differs")
+        grad_x2_warp = grad_x2_warp.contiguous()
+    _i32(B, C, H, W, input1.numel())
+    input1, x2, flow = input1.contiguous(), x2.contiguous(), flow.contiguous()
+    x2_warp, grad_corr = x2_warp.contiguous(), grad_corr.contiguous()
+    g1 = torch.empty_like(input1)
+    gx2 = torch.empty_like(x2)
+    gfl = torch.empty_like(flow)
+    if gfl.numel() == 0:
+        return g1, gx2, gfl
+    lib = _lib.load()
+    nws = lib.pwc_warp_corr_backward_workspace_size(B, C, H, W, pad_size, kernel_size,
+                                                    max_displacement, stride1, stride2, 0)
+    ws, wsp = _workspace(nws, input1.device)
+    cnt = _counters(B, input1.device)
+    _lib.check(lib.pwc_warp_corr_backward(
+        _ptr(input1), _ptr(x2), _ptr(flow), _ptr(x2_warp), _ptr(grad_corr),
+        _ptr(grad_x2_warp) if grad_x2_warp is not None else ctypes.c_void_p(0),
+        _ptr(g1), _ptr(gx2), _ptr(gfl), B, C, H, W, pad_size, kernel_size, max_displacement,
+        stride1, stride2, corr_multiply, 0, wsp, nws,
+        _ptr(cnt) if cnt is not None else ctypes.c_void_p(0), _stream(input1.device)),
+        "WarpCorrelation_backward")
+    del ws
+    return g1, gx2, gfl
+
+
 class WarpCorrelationFunction(Function):
     """autograd for model.py:80-83 as one op: outputs (corr, x2_warp).  Backward chains the
-    reference's two backward passes: correlation (cu:108-290) into the warped features, plus
-    any gradient arriving on x2_warp itself, then grid_sample's (warp_backward)."""
+    reference's two backward passes -- correlation (cu:108-290) into the warped features, plus
+    any gradient arriving on x2_warp itself, then grid_sample's -- as warp_corr_backward (one
+    launch at the coarse levels)."""
 
     @staticmethod
     def forward(ctx, input1, x2, flow, pad_size=9, kernel_size=1, max_displacement=9,
@@ -539,10 +605,10 @@ class WarpCorrelationFunction(Function):
     def backward(ctx, grad_corr, grad_x2w):
         input1, x2, flow, x2w = ctx.saved_tensors
         with torch.cuda.device(input1.device):
-            # unused outputs arrive as zeros (autograd materialises them)
-            g1, gw = corr_backward(input1, x2w, grad_corr, *ctx.args)
-            gw = gw + grad_x2w
-            gx2, gflow = warp_backward(x2, flow, gw)
+            # unused outputs arrive as zeros (autograd materialises them); fp16 / bf16 storage
+            # has no backward kernels (as corr_backward / warp_backward)
+            g1, gx2, gflow = warp_corr_backward(input1, x2, flow, x2w, grad_corr, *ctx.args,
+                                                grad_x2_warp=grad_x2w)
         return (g1, gx2, gflow) + (None,) * 6
 
 

@@ -4,8 +4,10 @@
 One step = for every correlated level l0..l4 (model.py:72-113): forward warp (modules.py:31-42)
 + Correlation (model.py:24), then the backward of both for an upstream gradient of the cost
 volume: Correlation backward (correlation_cuda_kernel.cu:108-290 -> d/dx1, d/dx2_warp), then
-WarpingLayer backward (ATen grid_sampler_2d_backward semantics -> d/dx2, d/dflow).  Each step
-is one hipGraph replay; inputs rotate past the Infinity Cache.
+WarpingLayer backward (ATen grid_sampler_2d_backward semantics -> d/dx2, d/dflow).  The fused
+levels (--fused-levels, default l0 and l1) run the pair as WarpCorrelation: one forward launch
+and one backward call (warp_corr_backward; WarpCorrelationFunction.backward).  Each step is one
+hipGraph replay; inputs rotate past the Infinity Cache.
 
 Headline ("value"): DEPENDENCY order -- level after level, each level's forward then its
 backward, nothing batched across levels.  The "grouped" object times the same step with the
@@ -36,7 +38,8 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from pwcnet_amd.ops import (corr_backward, corr_forward, corr_forward_group,  # noqa: E402
-                            warp_backward, warp_corr_forward, warp_corr_forward_group,
+                            warp_backward, warp_corr_backward, warp_corr_forward,
+                            warp_corr_forward_group,
                             warp_forward, warp_forward_group)
 
 OUTPUTS = ("corr", "g1", "gx2", "gfl")
@@ -54,7 +57,14 @@ def make_set(B, shapes, dev, gen):
     return s
 
 
-def backward_level(lv, x2w):
+def backward_level(lv, x2w, fused):
+    """The level's backward: fused levels (the forward was one WarpCorrelation launch) as ONE
+    warp_corr_backward call (WarpCorrelationFunction.backward), the others as the correlation
+    backward then the warp backward."""
+    if fused:
+        lv["g1"], lv["gx2"], lv["gfl"] = warp_corr_backward(lv["x1"], lv["x2"], lv["fl"], x2w,
+                                                            lv["gc"], **bench.CORR_ARGS)
+        return
     lv["g1"], g2w = corr_backward(lv["x1"], x2w, lv["gc"], **bench.CORR_ARGS)
     lv["gx2"], lv["gfl"] = warp_backward(lv["x2"], lv["fl"], g2w)
 
@@ -63,12 +73,13 @@ def step_dependency(s, fused):
     """Level after level: forward (fused levels as one WarpCorrelation launch that also emits
     x2_warp), then that level's backward."""
     for l, lv in enumerate(s):
-        if l in fused and l < len(s) - 1:
+        fl = l in fused and l < len(s) - 1
+        if fl:
             lv["corr"], x2w = warp_corr_forward(lv["x1"], lv["x2"], lv["fl"], **bench.CORR_ARGS)
         else:
             x2w = warp_forward(lv["x2"], lv["fl"])
             lv["corr"] = corr_forward(lv["x1"], x2w, **bench.CORR_ARGS)
-        backward_level(lv, x2w)
+        backward_level(lv, x2w, fl)
 
 
 def step_grouped(s, fused):
@@ -89,7 +100,7 @@ def step_grouped(s, fused):
         s[l]["corr"] = c
     s[last]["corr"] = corr_forward(s[last]["x1"], x2w[last], **bench.CORR_ARGS)
     for l, lv in enumerate(s):
-        backward_level(lv, x2w[l])
+        backward_level(lv, x2w[l], l in fl)
 
 
 def fresh(s):
@@ -143,10 +154,16 @@ def op_table(s, fused, reps=20):
             ops.append(("warp_fwd", (2 * C + 2) * hw4, lambda: warp_forward(lv["x2"], lv["fl"])))
             ops.append(("corr_fwd", (2 * C + 81) * hw4,
                         lambda: corr_forward(lv["x1"], x2w, **bench.CORR_ARGS)))
-        ops.append(("corr_bwd", (4 * C + 81) * hw4,
-                    lambda: corr_backward(lv["x1"], x2w, lv["gc"], **bench.CORR_ARGS)))
-        ops.append(("warp_bwd", (3 * C + 4) * hw4,
-                    lambda: warp_backward(lv["x2"], lv["fl"], g2w)))
+        if l in fused and l < last:
+            # reads x1, x2, x2_warp, 81 gradient planes, the flow; writes g1, gx2, grad_flow
+            ops.append(("warp_corr_bwd", (5 * C + 81 + 4) * hw4,
+                        lambda: warp_corr_backward(lv["x1"], lv["x2"], lv["fl"], x2w, lv["gc"],
+                                                   **bench.CORR_ARGS)))
+        else:
+            ops.append(("corr_bwd", (4 * C + 81) * hw4,
+                        lambda: corr_backward(lv["x1"], x2w, lv["gc"], **bench.CORR_ARGS)))
+            ops.append(("warp_bwd", (3 * C + 4) * hw4,
+                        lambda: warp_backward(lv["x2"], lv["fl"], g2w)))
         for name, nbytes, fn in ops:
             us = timed(fn)
             gbs = nbytes / (us * 1e-6) / 1e9
