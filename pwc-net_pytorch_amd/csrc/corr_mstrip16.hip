@@ -50,6 +50,15 @@ void take_launch_events(hipEvent_t* start, hipEvent_t* stop);  // capi.hip
 
 namespace mstrip16 {
 
+// volume store cache policy: 0 (write-back).  Nontemporal (2) stores wrote 86.1 MB per l4
+// launch for 74.3 MB of volume (partial lines streamed out twice); write-back stores write
+// 72.6 MB within the launch, the l4 kernel runs 3.79 -> 4.05 TB/s by its events, and config 4's
+// step is unchanged (102.19 K pairs/s both, 4 alternating rounds;
+// profiles/r06f_mstrip16_store_policy.txt).  Measurement builds may override.
+#ifndef PWC_MS_STPOL
+#define PWC_MS_STPOL 0
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -288,7 +297,8 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
 #pragma unroll
     for (int t = 0; t < NTJ; ++t)
       __builtin_amdgcn_raw_buffer_store_b128(
-          h, rso, (int)(lane_ok ? o0 + (uint32_t)((TJ0 + t) * 9 + jj) * pstep : kOOB), 0, 2);
+          h, rso, (int)(lane_ok ? o0 + (uint32_t)((TJ0 + t) * 9 + jj) * pstep : kOOB), 0,
+          PWC_MS_STPOL);
     return;
   }
   int sl = slot0 + TJ0;
@@ -349,7 +359,7 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
           : "+v"(p0), "+v"(p1), "+v"(q0), "+v"(q1));
       const u32x4 hs = {p0, p1, q0, q1};
       __builtin_amdgcn_raw_buffer_store_b128(hs, rso, (int)(lane_ok ? o0 + pl * pstep : kOOB), 0,
-                                             2);
+                                             PWC_MS_STPOL);
       if (t + 1 < NTJ) bc = bn;
       continue;
     }
@@ -365,8 +375,7 @@ __device__ __forceinline__ void tj_rows(const char* lds, int slot0, int lane_b,
                                                  (_Float16)fmaxf(e[1][v], e[1][v] * slope)});
     }
     const uint32_t off = o0 + pl * pstep;
-    // nontemporal: the volume is read by the next layer, not by this kernel
-    __builtin_amdgcn_raw_buffer_store_b128(h, rso, (int)(lane_ok ? off : kOOB), 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(h, rso, (int)(lane_ok ? off : kOOB), 0, PWC_MS_STPOL);
     if (t + 1 < NTJ) bc = bn;
   }
 }
