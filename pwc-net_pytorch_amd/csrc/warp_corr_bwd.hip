@@ -57,7 +57,8 @@ struct Args {
   float halfx, halfy, divisor;
   float inv_hw, inv_w, inv_wp, inv_pp;  // 1/d for qdiv
   int abl;  // measurement only (knob wcb_abl): 1 no correlation sums, 2 no lists / grad_x2,
-            // 4 no grad_flow reduction
+            // 4 no grad_flow reduction, 8 gO loads out of range (zeros), 16 no border clear,
+            // 32 no partial stores / arrival
 };
 
 __device__ __forceinline__ void lds_barrier() {
@@ -134,7 +135,7 @@ void warp_corr_bwd_small(Args a) {
   GT gq[NGO];
 #pragma unroll
   for (int j = 0; j < NGO; ++j) {
-    const unsigned off = (unsigned)((j * NT + t) * GV) * 4u;
+    const unsigned off = (a.abl & 8) ? 0x80000000u : (unsigned)((j * NT + t) * GV) * 4u;
     if constexpr (V4)
       gq[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)off, 0, 0));
     else
@@ -143,7 +144,7 @@ void warp_corr_bwd_small(Args a) {
   for (int i = t; i < NW * HW; i += NT) cnt[i] = 0;
   // the bordered planes' zero border (the interior is written below: no overlap) and gO's
   // guard pixels
-  for (int i = t; i < NQ * PP; i += NT) {
+  for (int i = t; i < ((a.abl & 16) ? 0 : NQ * PP); i += NT) {
     const int r = i - qdiv(i, a.inv_pp) * PP, ry = qdiv(r, a.inv_wp);
     const int yy = ry - 8, xx = r - ry * Wp - 8;
     if (yy < 0 || yy >= H || xx < 0 || xx >= W)
@@ -255,15 +256,17 @@ void warp_corr_bwd_small(Args a) {
       for (int j = 1; j < NQ; ++j) gix += red[j * HW + p], giy += red[NT + j * HW + p];
     }
     float* pp = a.part + ((size_t)(g * a.B + n) * 2) * plane;
-    __hip_atomic_store(pp + p, gix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(pp + plane + p, giy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!(a.abl & 32)) {
+      __hip_atomic_store(pp + p, gix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(pp + plane + p, giy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   // every partial store has completed (written through to the coherent level) before the
   // counter moves
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
   unsigned old = 0;
-  if (t == 0)
+  if (t == 0 && !(a.abl & 32))
     old = __hip_atomic_fetch_add(a.cnt + n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // g1: plain stores (the launcher requires C % (4 NQ) == 0)
   if (own) {
