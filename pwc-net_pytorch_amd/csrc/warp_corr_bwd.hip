@@ -404,12 +404,19 @@ size_t warp_corr_bwd_small_workspace(int B, int C, int H, int W) {
   return (size_t)ng * B * 2 * H * W * sizeof(float);
 }
 
-template <bool V4, int NGO>
-static const void* pick_nq(int nq) {
+// the reachable (gO load class, quads) instantiations: quads 4 need <= 64 pixels, 2 <= 128
+static const void* pick_kernel(int hw, int nq) {
   using namespace cbwd;
-  return nq == 4   ? reinterpret_cast<const void*>(&warp_corr_bwd_small<V4, NGO, 4>)
-         : nq == 2 ? reinterpret_cast<const void*>(&warp_corr_bwd_small<V4, NGO, 2>)
-                   : reinterpret_cast<const void*>(&warp_corr_bwd_small<V4, NGO, 1>);
+#define WCB_K(V, G, Q) reinterpret_cast<const void*>(&warp_corr_bwd_small<V, G, Q>)
+  const int gc = gload_class(hw);
+  if (hw % 4 == 0) {
+    if (gc == 7) return nq == 4 ? WCB_K(true, 7, 4) : nq == 2 ? WCB_K(true, 7, 2) : WCB_K(true, 7, 1);
+    if (gc == 14) return nq == 2 ? WCB_K(true, 14, 2) : WCB_K(true, 14, 1);
+    return WCB_K(true, 21, 1);
+  }
+  if (gc == 14) return nq == 4 ? WCB_K(false, 14, 4) : nq == 2 ? WCB_K(false, 14, 2) : WCB_K(false, 14, 1);
+  return nq == 4 ? WCB_K(false, 24, 4) : nq == 2 ? WCB_K(false, 24, 2) : WCB_K(false, 24, 1);
+#undef WCB_K
 }
 
 // hipErrorNotSupported: not this path (the caller runs the two launches)
@@ -446,10 +453,7 @@ hipError_t warp_corr_bwd_small(const void* in1, const void* x2, const void* flow
   a.inv_wp = 1.f / (float)(W + 16);
   a.inv_pp = 1.f / (float)((H + 16) * (W + 16));
   const size_t lds = (size_t)lds_floats(H, W, nq) * sizeof(float);
-  const int gc = gload_class(hw);
-  const void* f = hw % 4 == 0 ? (gc == 7 ? pick_nq<true, 7>(nq)
-                                 : gc == 14 ? pick_nq<true, 14>(nq) : pick_nq<true, 21>(nq))
-                              : (gc == 14 ? pick_nq<false, 14>(nq) : pick_nq<false, 24>(nq));
+  const void* f = pick_kernel(hw, nq);
   hipError_t e = lds_limit(f, (int)lds);
   if (e != hipSuccess) return e;
   void* args[] = {&a};

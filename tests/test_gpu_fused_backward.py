@@ -68,6 +68,27 @@ def test_warp_corr_backward_vs_oracle(shape, scale, extra):
     np.testing.assert_allclose(_np(gfl), rfl, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
 
 
+# one shape per instantiation of the one-launch kernel (16-B / scalar gO copy class x channel
+# quads per workgroup): (V4, loads, quads)
+INSTANTIATIONS = [(1, 16, 8, 8), (1, 8, 8, 8), (1, 4, 8, 8), (1, 8, 10, 12), (2, 128, 12, 14),
+                  (1, 12, 16, 16), (2, 192, 6, 7), (1, 8, 5, 3), (2, 4, 2, 3), (1, 16, 7, 7),
+                  (1, 8, 5, 13), (1, 4, 7, 7)]
+
+
+@pytest.mark.parametrize("shape", INSTANTIATIONS, ids=lambda s: "B{}C{}_{}x{}".format(*s))
+def test_warp_corr_backward_instantiations(shape):
+    """Every instantiation the one-launch dispatch can reach, against the oracle chain."""
+    from pwcnet_amd.ops import warp_corr_backward, warp_forward
+    B, C, H, W = shape
+    a, b, f, g, e = _case(3 * H + W + C, B, C, H, W, 2.0)
+    g1, gx2, gfl = warp_corr_backward(_t(a), _t(b), _t(f), warp_forward(_t(b), _t(f)), _t(g),
+                                      9, 1, 9, 1, 2, grad_x2_warp=_t(e))
+    r1, rx2, rfl = _oracle(a, b, f, g, e)
+    np.testing.assert_allclose(_np(g1), r1, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gx2), rx2, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gfl), rfl, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)))
+
+
 @pytest.mark.parametrize("shape", [(8, 192, 6, 7), (8, 128, 12, 14), (3, 16, 8, 10)],
                          ids=lambda s: "B{}C{}_{}x{}".format(*s))
 def test_warp_corr_backward_one_launch_vs_two(shape):

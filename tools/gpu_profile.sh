@@ -22,5 +22,8 @@ timeout -k 10 300 python tools/train_bench.py > $OUT/train.json 2> $OUT/train.er
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/train_trace -o run --output-format csv -- python tools/train_bench.py --grouped-mode off --no-kernels > $OUT/train_traced.json 2> $OUT/train_trace.err || { tail $OUT/train_trace.err; exit 1; }
 timeout -k 10 300 python bench.py --dtype fp16 --batch 16 --height 448 --width 1024 --no-cpu-baseline --no-net-forward > $OUT/cfg4.json 2> $OUT/cfg4.err || { tail $OUT/cfg4.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/cfg4_trace -o run --output-format csv -- python bench.py --dtype fp16 --batch 16 --height 448 --width 1024 --no-cpu-baseline --no-pmc --no-net-forward --no-corr4 --grouped-mode off > $OUT/cfg4_traced.json 2> $OUT/cfg4_trace.err || { tail $OUT/cfg4_trace.err; exit 1; }
-timeout -k 10 120 tools/strip_bench_census 300 > $OUT/strip_census.txt 2>&1 || { tail $OUT/strip_census.txt; exit 1; }
+# (the strip census binary is a local measurement build; it does not travel with the tree)
+if [ -x tools/strip_bench_census ]; then
+  timeout -k 10 120 tools/strip_bench_census 300 > $OUT/strip_census.txt 2>&1 || { tail $OUT/strip_census.txt; exit 1; }
+fi
 echo done
