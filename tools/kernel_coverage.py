@@ -23,7 +23,7 @@ def so_kernels(path):
         name = parts[2]
         if name.startswith("void "):
             name = name[5:]
-        if name.startswith("pwc::") and not re.search(r"attr|guard|spec|::g_", name):
+        if name.startswith("pwc::") and not re.search(r"attr|guard|spec|::g_|lds_limit", name):
             names.add(name)
     return names
 
