@@ -34,7 +34,8 @@
 namespace pwc {
 namespace cbwd {
 
-constexpr int NT = 256;    // threads = maximum image pixels
+constexpr int NT = 512;    // threads: up to three displacement-row groups of (quad, pixel)
+constexpr int MAXP = 256;  // quads x pixels per group (one thread each)
 constexpr int D = 9;       // displacements per axis
 constexpr int ND = D * D;  // cost-volume planes
 constexpr int NW = NT / 64;
@@ -55,7 +56,8 @@ struct Args {
   unsigned* cnt;      // [B] arrival counters (zero before and after)
   int B, C, H, W, ng;
   float halfx, halfy, divisor;
-  float inv_hw, inv_w, inv_wp, inv_pp;  // 1/d for qdiv
+  float inv_hw, inv_w, inv_wp, inv_pp, inv_qhw;  // 1/d for qdiv
+  int ntg;  // displacement-row groups (thread groups splitting the 9 rows)
   int abl;  // measurement only (knob wcb_abl): 1 no correlation sums, 2 no lists / grad_x2,
             // 4 no grad_flow reduction, 8 gO loads out of range (zeros), 16 no border clear,
             // 32 no partial stores / arrival
@@ -71,17 +73,21 @@ __device__ __forceinline__ int qdiv(int x, float inv) { return (int)(((float)x +
 
 // LDS floats: gO pixel-major (81 per pixel) with 8 zero guard pixels each side, x1 / x2_warp
 // as NQ zero-bordered planes of float4 quads ((H + 16) x (W + 16): every displacement of an
-// in-image pixel lands inside), x2 / gw as NQ plain quad planes, per-wave slot counters, list
-// starts / lengths, list pixels and weights (4 per source pixel), a [2][NT] reduction buffer,
-// the arrival broadcast
+// in-image pixel lands inside), x2 / gw as NQ plain quad planes, the other displacement-row
+// groups' partial sums ([2 groups][2][NQ HW] quads), per-wave slot counters, list starts /
+// lengths, list pixels and weights (4 per source pixel), a [2][NT] reduction buffer, the
+// arrival broadcast
 __host__ __device__ constexpr int lds_floats(int h, int w, int nq) {
   return ((ND * (h * w + 16) + 3) & ~3) + 2 * 4 * nq * (h + 16) * (w + 16) + 2 * 4 * nq * h * w +
-         NW * h * w + 2 * h * w + 2 * 4 * h * w + 2 * NT + 4;
+         16 * nq * h * w + NW * h * w + 2 * h * w + 2 * 4 * h * w + 2 * NT + 4;
 }
 
 // V4: gO copied in 16-B loads (HW % 4 == 0); NGO: gO loads per thread (all in flight at once;
-// those past the end read zeros from the range check); NQ: channel quads per workgroup (thread
-// t = (quad t / HW, pixel t % HW): NQ * HW <= NT).
+// those past the end read zeros from the range check); NQ: channel quads per workgroup.  Thread
+// t = (displacement-row group t / (NQ HW), quad, pixel): the ntg <= 3 groups each sum a third
+// (or half) of the 9 displacement rows -- the sums' dependent chain is the kernel's longest
+// phase, and one (quad, pixel) per thread leaves most SIMDs with one wave -- and group 0 adds the
+// others' partial sums in group order, then carries on alone.
 // (one or two waves per SIMD: registers for a whole displacement row's reads in flight -- at
 // the default occupancy target the scheduler waited for each term's reads in turn)
 template <bool V4, int NGO, int NQ>
@@ -99,7 +105,8 @@ void warp_corr_bwd_small(Args a) {
   f32x4* f2p = f1p + NQ * PP;
   f32x4* xq = f2p + NQ * PP;                       // [NQ][HW]
   f32x4* gwq = xq + NQ * HW;
-  int* cnt = reinterpret_cast<int*>(gwq + NQ * HW);  // [NW][HW]
+  f32x4* comb = gwq + NQ * HW;                     // [2 groups][2][NQ * HW]
+  int* cnt = reinterpret_cast<int*>(comb + 4 * NQ * HW);  // [NW][HW]
   int* sst = cnt + NW * HW;                          // list start / length per pixel
   int* sln = sst + HW;
   int* lp = sln + HW;                                // [4 * HW] source pixel of a list entry
@@ -107,11 +114,15 @@ void warp_corr_bwd_small(Args a) {
   float* red = lw + 4 * HW;                          // [2][NT]
   int* arrival = reinterpret_cast<int*>(red + 2 * NT);
   const unsigned plane = (unsigned)HW;
-  const int k = qdiv(t, a.inv_hw);  // this thread's channel quad
-  const bool own = k < NQ;
-  const int p = own ? t - k * HW : 0;
-  const int kq = own ? k * HW : 0;  // quad plane offsets in LDS
-  const int kp = own ? k * PP : 0;
+  const int qhw = NQ * HW;
+  const int tg = qdiv(t, a.inv_qhw), rq = t - tg * qhw;  // displacement-row group, (quad, pixel)
+  const int k = qdiv(rq, a.inv_hw);                     // this thread's channel quad
+  const bool act = tg < a.ntg;  // sums a share of the displacements
+  const bool own = t < qhw;     // group 0: the (quad, pixel) owner
+  const bool pix0 = t < HW;     // group 0, quad 0: one thread per pixel (lists, scan)
+  const int p = act ? rq - k * HW : 0;
+  const int kq = act ? k * HW : 0;  // quad plane offsets in LDS
+  const int kp = act ? k * PP : 0;
   const int py = qdiv(p, a.inv_w), px = p - py * W;
 
   // ---- every load first: flow, the quad's channels, the gradient on x2_warp, gO ----
@@ -195,8 +206,10 @@ void warp_corr_bwd_small(Args a) {
   // so every term is added (outside ones are exact zeros) and all offsets inside a
   // displacement row are compile-time: a row's 36 LDS reads go out back to back
   f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  const int tjlo = act ? (tg * D + a.ntg / 2) / a.ntg : 0;
+  const int tjhi = act ? ((tg + 1) * D + a.ntg / 2) / a.ntg : 0;
 #pragma unroll 1
-  for (int tj = 0; tj < ((a.abl & 1) ? 0 : D); ++tj) {
+  for (int tj = tjlo; tj < ((a.abl & 1) ? tjlo : tjhi); ++tj) {
     const int dy = 2 * tj - 8;
     const bool r2 = py - dy >= 0 && py - dy < H;
     const int dyr = r2 ? dy : 0;
@@ -217,6 +230,18 @@ void warp_corr_bwd_small(Args a) {
     for (int ti = 0; ti < D; ++ti) {
       s1 += a1[ti] * b1[ti];
       s2 += a2[ti] * b2[ti];
+    }
+  }
+  // the other groups' shares, added in group order
+  if (act && tg > 0) {
+    comb[(2 * (tg - 1)) * qhw + rq] = s1;
+    comb[(2 * (tg - 1) + 1) * qhw + rq] = s2;
+  }
+  lds_barrier();
+  if (own) {
+    for (int g2 = 1; g2 < a.ntg; ++g2) {
+      s1 += comb[(2 * (g2 - 1)) * qhw + t];
+      s2 += comb[(2 * (g2 - 1) + 1) * qhw + t];
     }
   }
   f32x4 gw;
@@ -245,12 +270,12 @@ void warp_corr_bwd_small(Args a) {
   int rank[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    rank[j] = k == 0 && slot[j] >= 0 ? atomicAdd(&cnt[wave * HW + slot[j]], 1) : 0;
+    rank[j] = pix0 && slot[j] >= 0 ? atomicAdd(&cnt[wave * HW + slot[j]], 1) : 0;
   if (NQ > 1) lds_barrier();
   // the workgroup's partial of grad_flow[p] (quads in order), out first: the arrival counter
   // moves once every partial has landed, and its round trip then runs under the list build
   // and the grad_x2 gathers
-  if (k == 0) {
+  if (pix0) {
     if (NQ > 1) {
 #pragma unroll
       for (int j = 1; j < NQ; ++j) gix += red[j * HW + p], giy += red[NT + j * HW + p];
@@ -279,7 +304,7 @@ void warp_corr_bwd_small(Args a) {
   int wc[NW], len = 0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
-    wc[w] = k == 0 ? cnt[w * HW + p] : 0;
+    wc[w] = pix0 ? cnt[w * HW + p] : 0;
     len += wc[w];
   }
   int incl = len;
@@ -291,7 +316,7 @@ void warp_corr_bwd_small(Args a) {
   if ((t & 63) == 63) wsum[wave] = incl;
   lds_barrier();
   for (int w = 0; w < wave; ++w) incl += wsum[w];
-  if (k == 0) {
+  if (pix0) {
     int run = incl - len;
     sst[p] = run;
     sln[p] = len;
@@ -304,7 +329,7 @@ void warp_corr_bwd_small(Args a) {
   lds_barrier();
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    if (k == 0 && slot[j] >= 0) {
+    if (pix0 && slot[j] >= 0) {
       const int e = cnt[wave * HW + slot[j]] + rank[j];
       lp[e] = p;
       lw[e] = wk[j];
@@ -377,24 +402,25 @@ hipError_t add_inplace_f32(void* y, const void* x, size_t n, hipStream_t stream)
 static int gload_class(long long hw) {
   if (hw % 4 == 0) {
     const long long n = (cbwd::ND * hw + 4 * cbwd::NT - 1) / (4 * cbwd::NT);
-    return n <= 7 ? 7 : n <= 14 ? 14 : n <= 21 ? 21 : 0;
+    return n <= 4 ? 4 : n <= 7 ? 7 : n <= 11 ? 11 : 0;
   }
   const long long n = (cbwd::ND * hw + cbwd::NT - 1) / cbwd::NT;
-  return n <= 14 ? 14 : n <= 24 ? 24 : 0;
+  return n <= 7 ? 7 : n <= 12 ? 12 : 0;
 }
 
 // channel quads per workgroup: the most that fit one thread per (quad, pixel) and divide C
 static int quads(int C, long long hw) {
   for (int nq : {4, 2, 1})
-    if (nq * hw <= cbwd::NT && C % (4 * nq) == 0) return nq;
+    if (nq * hw <= cbwd::MAXP && C % (4 * nq) == 0) return nq;
   return 0;
 }
 
 bool warp_corr_bwd_small_accepts(int B, int C, int H, int W) {
   using namespace cbwd;
   const long long hw = (long long)H * W;
-  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || hw > NT || quads(C, hw) == 0) return false;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || hw > MAXP || quads(C, hw) == 0) return false;
   if ((long long)B * C * hw >= (1ll << 31) || gload_class(hw) == 0) return false;
+  if ((long long)lds_floats(H, W, quads(C, hw)) * 4 > 160 * 1024) return false;  // LDS
   return debug_knob("warp_corr_bwd", 1) != 0;
 }
 
@@ -409,13 +435,14 @@ static const void* pick_kernel(int hw, int nq) {
   using namespace cbwd;
 #define WCB_K(V, G, Q) reinterpret_cast<const void*>(&warp_corr_bwd_small<V, G, Q>)
   const int gc = gload_class(hw);
-  if (hw % 4 == 0) {
-    if (gc == 7) return nq == 4 ? WCB_K(true, 7, 4) : nq == 2 ? WCB_K(true, 7, 2) : WCB_K(true, 7, 1);
-    if (gc == 14) return nq == 2 ? WCB_K(true, 14, 2) : WCB_K(true, 14, 1);
-    return WCB_K(true, 21, 1);
+  if (hw % 4 == 0) {  // 16-B copy: <= 100 / 176 / 256 pixels
+    if (gc == 4) return nq == 4 ? WCB_K(true, 4, 4) : nq == 2 ? WCB_K(true, 4, 2) : WCB_K(true, 4, 1);
+    if (gc == 7) return nq == 2 ? WCB_K(true, 7, 2) : WCB_K(true, 7, 1);
+    return WCB_K(true, 11, 1);
   }
-  if (gc == 14) return nq == 4 ? WCB_K(false, 14, 4) : nq == 2 ? WCB_K(false, 14, 2) : WCB_K(false, 14, 1);
-  return nq == 4 ? WCB_K(false, 24, 4) : nq == 2 ? WCB_K(false, 24, 2) : WCB_K(false, 24, 1);
+  // scalar copy: <= 44 / 75 pixels
+  if (gc == 7) return nq == 4 ? WCB_K(false, 7, 4) : nq == 2 ? WCB_K(false, 7, 2) : WCB_K(false, 7, 1);
+  return nq == 4 ? WCB_K(false, 12, 4) : nq == 2 ? WCB_K(false, 12, 2) : WCB_K(false, 12, 1);
 #undef WCB_K
 }
 
@@ -452,6 +479,8 @@ hipError_t warp_corr_bwd_small(const void* in1, const void* x2, const void* flow
   a.inv_w = 1.f / (float)W;
   a.inv_wp = 1.f / (float)(W + 16);
   a.inv_pp = 1.f / (float)((H + 16) * (W + 16));
+  a.inv_qhw = 1.f / (float)(nq * hw);
+  a.ntg = NT / (nq * hw) < 3 ? NT / (nq * hw) : 3;
   const size_t lds = (size_t)lds_floats(H, W, nq) * sizeof(float);
   const void* f = pick_kernel(hw, nq);
   hipError_t e = lds_limit(f, (int)lds);

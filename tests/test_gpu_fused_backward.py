@@ -16,8 +16,9 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
-# (B, C, H, W): one launch (l0, l1, a 16-B-copy shape, tiny images, 256 pixels) and two launches
-# (l2: too many pixels; C % 4 != 0; 99 pixels not a multiple of 4 past the scalar-copy limit)
+# (B, C, H, W): one launch (l0, l1, a 16-B-copy shape, tiny images) and two launches (256
+# pixels: LDS; l2: too many pixels; C % 4 != 0; 99 pixels not a multiple of 4 past the
+# scalar-copy limit)
 SHAPES = [(2, 192, 6, 7), (2, 128, 12, 14), (3, 16, 8, 10), (1, 8, 5, 3), (2, 4, 2, 3),
           (1, 12, 16, 16), (2, 96, 24, 28), (1, 6, 7, 9), (1, 8, 9, 11)]
 
@@ -71,7 +72,7 @@ def test_warp_corr_backward_vs_oracle(shape, scale, extra):
 # one shape per instantiation of the one-launch kernel (16-B / scalar gO copy class x channel
 # quads per workgroup): (V4, loads, quads)
 INSTANTIATIONS = [(1, 16, 8, 8), (1, 8, 8, 8), (1, 4, 8, 8), (1, 8, 10, 12), (2, 128, 12, 14),
-                  (1, 12, 16, 16), (2, 192, 6, 7), (1, 8, 5, 3), (2, 4, 2, 3), (1, 16, 7, 7),
+                  (1, 12, 12, 16), (2, 192, 6, 7), (1, 8, 5, 3), (2, 4, 2, 3), (1, 16, 7, 7),
                   (1, 8, 5, 13), (1, 4, 7, 7)]
 
 
