@@ -17,10 +17,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 # (B, C, H, W): one launch (l0, l1, a 16-B-copy shape, tiny images) and two launches (256
-# pixels: LDS; l2: too many pixels; C % 4 != 0; 99 pixels not a multiple of 4 past the
+# pixels: LDS; l2 and other larger images; C % 4 != 0; 99 pixels not a multiple of 4 past the
 # scalar-copy limit)
 SHAPES = [(2, 192, 6, 7), (2, 128, 12, 14), (3, 16, 8, 10), (1, 8, 5, 3), (2, 4, 2, 3),
-          (1, 12, 16, 16), (2, 96, 24, 28), (1, 6, 7, 9), (1, 8, 9, 11)]
+          (1, 12, 16, 16), (2, 96, 24, 28), (1, 8, 20, 20), (1, 4, 17, 20), (1, 6, 7, 9),
+          (1, 8, 9, 11), (1, 4, 32, 24)]
 
 
 def _t(a):

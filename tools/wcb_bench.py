@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Level backward of the fused levels (config 5's l0 / l1, B = 8): the one-launch
+"""Level backward of config 5's l0 / l1 / l2 (B = 8): the one-launch
 warp_corr_backward against the two-launch path (corr_backward + warp_backward), each timed as
 20 back-to-back calls replayed from one hipGraph (event-timed, us per call), for the knob
 settings given (PWC_DEBUG syntax; "-" = defaults).
@@ -45,7 +45,7 @@ def main():
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev).manual_seed(3)
     B = 8
-    for l, (C, h, w) in enumerate(bench.level_shapes(384, 448)[:2]):
+    for l, (C, h, w) in enumerate(bench.level_shapes(384, 448)[:3]):
         x1 = torch.randn(B, C, h, w, device=dev, generator=gen)
         x2 = torch.randn(B, C, h, w, device=dev, generator=gen)
         fl = torch.randn(B, 2, h, w, device=dev, generator=gen) * 2
