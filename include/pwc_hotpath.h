@@ -62,7 +62,8 @@ extern "C" {
 /* ABI version; bumped on any signature change (2: workspace entry points, 3: timing hook,
  * 4: fused warp -> correlation, 5: fused flow upsample -> warp, corr into a slice,
  * 6: pwc_set_debug, 7: grouped warp / warp -> correlation launches, 8: one-launch warp
- * backward with a workspace, 9: pwc_corr_forward_plan, 10: pwc_corr_backward_plan). */
+ * backward with a workspace, 9: pwc_corr_forward_plan, 10: pwc_corr_backward_plan,
+ * 11: pwc_warp_corr_backward). */
 PWC_API int pwc_abi_version(void);
 
 /* Which kernel family pwc_corr_forward would launch for these arguments (the same dispatch
@@ -198,7 +199,7 @@ PWC_API int pwc_warp_backward(const void* x, const void* flow, const void* grad_
                       void* grad_flow, int B, int C, int H, int W, int dtype, void* stream);
 /* Same result with a caller-owned device workspace of at least
  * pwc_warp_backward_workspace_size() bytes (no initialisation needed).  On wide images
- * (W >= 96: the l4 level) grad_x and grad_flow come from one tile kernel -- per 16x16 tile of
+ * (W >= 56: the l3 / l4 levels) grad_x and grad_flow come from one tile kernel -- per 16x16 tile of
  * grad_x its output pixels' lists (fixed order) with x and grad_out streamed through LDS --
  * plus a small kernel that adds the channel groups' grad_flow partials (fixed order) and the
  * rare corners beyond the tiles' 8-pixel margins (fp32 atomics).  Other sizes, or a NULL /
