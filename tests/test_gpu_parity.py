@@ -241,6 +241,39 @@ def test_warp_backward_one_launch_vs_oracle(shape, scale):
                                    equal_nan=True)
 
 
+@pytest.mark.parametrize("scale", [2.0, 25.0])
+@pytest.mark.parametrize("shape", [(2, 96, 24, 28), (8, 96, 24, 28), (1, 40, 12, 40),
+                                   (1, 16, 12, 48), (1, 32, 12, 48), (1, 64, 10, 50)],
+                         ids=lambda s: "B{}C{}_{}x{}".format(*s))
+def test_warp_backward_whole_image_candidates(shape, scale):
+    """Images of <= 768 pixels (l2): every pixel is a candidate of every grad_x tile, so there
+    is no far-corner pass -- against the oracle (flows far beyond the 8-px margins included),
+    repeatable bit for bit (no atomics left), and within fp32 summation order of the margin
+    windows + far pass (PWC_DEBUG warp_bwd_whole=0).  One shape per instantiation."""
+    from pwcnet_amd import _lib
+    from pwcnet_amd.ops import warp_backward
+    B, C, H, W = shape
+    rng = np.random.default_rng(int(scale) * 3 + W)
+    x, g = _rand(rng, B, C, H, W), _rand(rng, B, C, H, W)
+    f = (rng.standard_normal((B, 2, H, W)) * scale).astype(np.float32)
+    gx, gf = warp_backward(_t(x), _t(f), _t(g))
+    gx1, gf1 = warp_backward(_t(x), _t(f), _t(g))
+    _lib.set_debug("warp_bwd_whole=0")
+    try:
+        gx0, gf0 = warp_backward(_t(x), _t(f), _t(g))
+    finally:
+        _lib.set_debug("")
+    torch.cuda.synchronize()
+    assert torch.equal(gx, gx1) and torch.equal(gf.nan_to_num(), gf1.nan_to_num())
+    np.testing.assert_allclose(_np(gx), _np(gx0), rtol=1e-6, atol=1e-6)
+    assert torch.equal(gf.nan_to_num(), gf0.nan_to_num())  # the same grad_flow code
+    if x.size <= 2 * 96 * 24 * 28:
+        rx, rf = O.warp_backward(x, f, g)
+        np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)),
+                                   equal_nan=True)
+
+
 def test_warp_backward_one_launch_repeatable():
     """No far corners -> no atomics: two calls agree bit for bit (fixed list and group order)."""
     from pwcnet_amd.ops import warp_backward
