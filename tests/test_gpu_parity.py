@@ -243,7 +243,7 @@ def test_warp_backward_one_launch_vs_oracle(shape, scale):
 
 @pytest.mark.parametrize("scale", [2.0, 25.0])
 @pytest.mark.parametrize("shape", [(2, 96, 24, 28), (8, 96, 24, 28), (1, 40, 12, 40),
-                                   (1, 16, 12, 48), (1, 32, 12, 48), (1, 64, 10, 50)],
+                                   (1, 8, 12, 48), (1, 32, 12, 48), (1, 64, 10, 50)],
                          ids=lambda s: "B{}C{}_{}x{}".format(*s))
 def test_warp_backward_whole_image_candidates(shape, scale):
     """Images of <= 768 pixels (l2): every pixel is a candidate of every grad_x tile, so there
@@ -272,6 +272,22 @@ def test_warp_backward_whole_image_candidates(shape, scale):
         np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)),
                                    equal_nan=True)
+
+
+@pytest.mark.parametrize("scale", [2.0, 25.0])
+def test_warp_backward_margin_windows_merged(scale):
+    """Images over 768 pixels keep the 8-px margin windows and the far pass after the merged
+    launch (here 8 x 32 tiles, two grad_flow channel groups): against the oracle."""
+    from pwcnet_amd.ops import warp_backward
+    B, C, H, W = 1, 24, 30, 40
+    rng = np.random.default_rng(int(scale) + 5)
+    x, g = _rand(rng, B, C, H, W), _rand(rng, B, C, H, W)
+    f = (rng.standard_normal((B, 2, H, W)) * scale).astype(np.float32)
+    gx, gf = warp_backward(_t(x), _t(f), _t(g))
+    rx, rf = O.warp_backward(x, f, g)
+    np.testing.assert_allclose(_np(gx), rx, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gf), rf, rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(C)),
+                               equal_nan=True)
 
 
 def test_warp_backward_one_launch_repeatable():
