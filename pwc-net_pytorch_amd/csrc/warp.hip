@@ -607,11 +607,19 @@ __global__ __launch_bounds__(256) void warp_bwd_far(const float* __restrict__ fl
 
 
 template <typename T>
+hipError_t warp_forward_win_t(const void*, const void*, void*, int, int, int, int, hipStream_t);
+
+template <typename T>
 hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int C, int H,
                           int W, hipStream_t stream) {
   const size_t npix = (size_t)B * H * W;
   if (npix == 0 || C == 0) return hipSuccess;
   if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
+  // large grids: the LDS-window kernel (warp_fwd_win.hip) where it takes the shape
+  if (npix >= 16384) {
+    const hipError_t e = warp_forward_win_t<T>(x, flow, out, B, C, H, W, stream);
+    if (e != hipErrorNotSupported) return e;
+  }
   const float halfx = (float)((W - 1.0) / 2.0), halfy = (float)((H - 1.0) / 2.0);
   const unsigned gx = (unsigned)((npix + 255) / 256);
 #define PWC_WARP_LAUNCH(CB, NG, XCD)                                                          \
