@@ -206,22 +206,26 @@ __global__ __launch_bounds__(NT) void warp_fwd_win(const T* __restrict__ x,
 // The window path of warp_forward_t (large grids).  Measured (tools/kbench.py --ops warp,
 // graph-replayed, profiles/r06k_warp_fwd_window.txt): config 4 (fp16, B = 16, 448 x 1024)
 // l2 / l3 / l4 8.5 / 16.9 / 29.9 -> 7.6 / 12.7 / 20.8 us with 8-row tiles and 4-channel chunks;
-// fp32 (config 2 l3 / l4) 5.7 / 9.0 -> 6.1 / 8.9 -- not taken by default.  hipErrorNotSupported
-// when it declines (fp32 unless knob warp_win = 2; rows not a whole number of 16-byte quads; a
-// plane too large for one buffer resource; fewer than 64 tiles; knob warp_win = 0) -- the caller
-// then runs warp_fwd_kernel.
+// fp32 (config 2 l3 / l4, 2-channel chunks) 5.7 / 9.0 -> 6.1 / 8.9 -- fp32 keeps the gathers and
+// this kernel is instantiated for 16-bit storage only.  hipErrorNotSupported when it declines
+// (fp32; rows not a whole number of 16-byte quads; a plane too large for one buffer resource;
+// fewer than 64 tiles unless knob warp_win = 2; knob warp_win = 0) -- the caller then runs
+// warp_fwd_kernel.
 template <typename T>
 hipError_t warp_forward_win_t(const void* x, const void* flow, void* out, int B, int C, int H,
                               int W, hipStream_t stream) {
+  if constexpr (sizeof(T) == 4) {
+    return hipErrorNotSupported;
+  } else {
   using namespace wwin;
   constexpr int Q = 16 / (int)sizeof(T);
   const int mode = debug_knob("warp_win", 1);
-  if (mode == 0 || (mode == 1 && sizeof(T) == 4)) return hipErrorNotSupported;
+  if (mode == 0) return hipErrorNotSupported;
   if (W % Q != 0 || B <= 0 || C <= 0 || H <= 0) return hipErrorNotSupported;
   if ((size_t)C * H * W * sizeof(T) >= (1ull << 31)) return hipErrorNotSupported;
   // tile width: 56 where it divides the row and 64 does not (W = 112, 56), else 64
   const bool t56 = W % 56 == 0 && W % 64 != 0;
-  constexpr int TH = 8, CC = sizeof(T) == 4 ? 2 : 4;
+  constexpr int TH = 8, CC = 4;
   const int TW = t56 ? 56 : 64;
   const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
   const int ntiles = ntx * nty;
@@ -250,6 +254,7 @@ hipError_t warp_forward_win_t(const void* x, const void* flow, void* out, int B,
     PWC_WIN(64);
 #undef PWC_WIN
   return hipGetLastError();
+  }
 }
 
 template hipError_t warp_forward_win_t<float>(const void*, const void*, void*, int, int, int, int,

@@ -1,7 +1,8 @@
-"""The LDS-window forward warp (csrc/warp_fwd_win.hip) against the gather kernel it replaces on
-large grids (warp_fwd_kernel, knob warp_win=0) -- bit for bit, fp32 / fp16 / bf16 -- and against
-the oracle (WarpingLayer, modules.py:31-42).  Flows beyond the 8-px window margin take the
-global-gather branch: covered by the large-flow cases."""
+"""The LDS-window forward warp (csrc/warp_fwd_win.hip, 16-bit storage) against the gather kernel
+it replaces on large grids (warp_fwd_kernel, knob warp_win=0) -- bit for bit, fp16 / bf16 -- and
+against the oracle (WarpingLayer, modules.py:31-42).  Flows beyond the 8-px window margin take
+the global-gather branch: covered by the large-flow cases.  fp32 keeps the gather kernel (the
+window measured no faster there, profiles/r06k_warp_fwd_window.txt)."""
 import numpy as np
 import pytest
 import torch
@@ -12,7 +13,7 @@ from pwcnet_amd.ops import warp_forward
 
 pytestmark = pytest.mark.gpu
 
-DT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+DT = {"fp16": torch.float16, "bf16": torch.bfloat16}
 
 # (B, C, H, W): config 2 l3 / l4 (56-px tiles), config-4 widths (64-px tiles), ragged edges
 # (H not a multiple of the tile height, W a multiple of 8 but not of the tile width), C not a
@@ -38,18 +39,17 @@ def _warp(x, f, knobs):
 
 
 def _both(x, f):
-    """(window kernel forced on every shape and storage type, gather kernel)."""
+    """(window kernel forced on every shape, gather kernel)."""
     return _warp(x, f, "warp_win=2"), _warp(x, f, "warp_win=0")
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp16", "bf16"])
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("scale", [0.0, 2.0, 12.0])
 def test_window_warp_bitwise_equals_gather_kernel(shape, scale, dtype):
     x, f = _inputs(shape, scale, dtype, seed=sum(shape) + int(scale))
     a, b = _both(x, f)
-    assert torch.equal(a.view(torch.int16 if dtype != "fp32" else torch.int32),
-                       b.view(torch.int16 if dtype != "fp32" else torch.int32))
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))
 
 
 @pytest.mark.parametrize("wgs", [1, 256, 100000])
@@ -71,20 +71,22 @@ def test_window_warp_default_dispatch():
 def test_window_warp_non_finite_flows():
     """NaN / inf / huge flows: the same output as the gather kernel (every such sample leaves the
     window and takes the global branch, where both kernels clamp and mask alike)."""
-    x, f = _inputs((1, 8, 64, 128), 2.0, "fp32", seed=7)
+    x, f = _inputs((1, 8, 64, 128), 2.0, "fp16", seed=7)
     f[0, 0, 3, 5] = float("nan")
     f[0, 1, 10, 20] = float("inf")
-    f[0, 0, 30, 40] = -1e30
-    f[0, 1, 50, 100] = 1e9
+    f[0, 0, 30, 40] = -60000.0
+    f[0, 1, 50, 100] = float("-inf")
     a, b = _both(x, f)
-    assert torch.equal(torch.nan_to_num(a, nan=7.0), torch.nan_to_num(b, nan=7.0))
+    assert torch.equal(torch.nan_to_num(a.float(), nan=7.0), torch.nan_to_num(b.float(), nan=7.0))
 
 
 @pytest.mark.parametrize("scale", [2.0, 20.0])
 def test_window_warp_vs_oracle(scale):
+    """fp16 storage: the oracle on the same fp16 values in fp64, within the output's rounding."""
     B, C, H, W = 2, 8, 48, 64
     rng = np.random.default_rng(11)
-    x = rng.standard_normal((B, C, H, W)).astype(np.float32)
-    f = (rng.standard_normal((B, 2, H, W)) * scale).astype(np.float32)
-    out = warp_forward(torch.from_numpy(x).cuda(), torch.from_numpy(f).cuda())
-    np.testing.assert_allclose(out.cpu().numpy(), O.warp_forward(x, f), rtol=1e-5, atol=1e-5)
+    x = rng.standard_normal((B, C, H, W)).astype(np.float16)
+    f = (rng.standard_normal((B, 2, H, W)) * scale).astype(np.float16)
+    out = _warp(torch.from_numpy(x).cuda(), torch.from_numpy(f).cuda(), "warp_win=2")
+    ref = O.warp_forward(x.astype(np.float32), f.astype(np.float32))
+    np.testing.assert_allclose(out.float().cpu().numpy(), ref, rtol=2e-3, atol=2e-3)
