@@ -243,7 +243,7 @@ def test_warp_backward_one_launch_vs_oracle(shape, scale):
 
 @pytest.mark.parametrize("scale", [2.0, 25.0])
 @pytest.mark.parametrize("shape", [(2, 96, 24, 28), (8, 96, 24, 28), (1, 40, 12, 40),
-                                   (1, 8, 12, 48), (1, 32, 12, 48), (1, 64, 10, 50)],
+                                   (1, 8, 12, 48), (1, 16, 12, 48), (1, 32, 12, 48), (1, 64, 10, 50)],
                          ids=lambda s: "B{}C{}_{}x{}".format(*s))
 def test_warp_backward_whole_image_candidates(shape, scale):
     """Images of <= 768 pixels (l2): every pixel is a candidate of every grad_x tile, so there
