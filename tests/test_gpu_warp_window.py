@@ -16,10 +16,10 @@ pytestmark = pytest.mark.gpu
 DT = {"fp16": torch.float16, "bf16": torch.bfloat16}
 
 # (B, C, H, W): config 2 l3 / l4 (56-px tiles), config-4 widths (64-px tiles), ragged edges
-# (H not a multiple of the tile height, W a multiple of 8 but not of the tile width), C not a
-# multiple of the channel slice
+# (H not a multiple of the tile height, W a multiple of 8 but not of the tile width, images
+# narrower than one tile), C not a multiple of the channel slice
 SHAPES = [(8, 32, 96, 112), (8, 64, 48, 56), (2, 32, 112, 256), (2, 96, 28, 64),
-          (1, 5, 40, 120), (2, 12, 33, 72), (1, 3, 130, 200)]
+          (1, 5, 40, 120), (2, 12, 33, 72), (1, 3, 130, 200), (2, 16, 20, 8), (1, 4, 9, 16)]
 
 
 def _inputs(shape, scale, dtype, seed):
