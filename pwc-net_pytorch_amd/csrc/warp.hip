@@ -615,8 +615,9 @@ hipError_t warp_forward_t(const void* x, const void* flow, void* out, int B, int
   const size_t npix = (size_t)B * H * W;
   if (npix == 0 || C == 0) return hipSuccess;
   if (npix * (size_t)(C > 2 ? C : 2) >= (1ull << 31)) return hipErrorInvalidValue;
-  // large grids: the LDS-window kernel (warp_fwd_win.hip) where it takes the shape
-  if (npix >= 16384) {
+  // large grids: the LDS-window kernel (warp_fwd_win.hip) where it takes the shape (knob
+  // warp_win = 2: any grid, for tests and measurement)
+  if (npix >= 16384 || debug_knob("warp_win", 1) == 2) {
     const hipError_t e = warp_forward_win_t<T>(x, flow, out, B, C, H, W, stream);
     if (e != hipErrorNotSupported) return e;
   }
